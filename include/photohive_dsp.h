@@ -1,0 +1,190 @@
+/* photohive_dsp.h -- C-ABI of PhotoHive_DSP_lib/libreport_data.so (MI355X build).
+ *
+ * Drop-in for the reference's libreport_data.so: the three legacy entry points
+ * keep their exact signatures and struct layouts, so the reference's own
+ * ctypes binding (/root/reference/lib.py:20-37, structures.py:6-106) loads
+ * this library unchanged.  Behind them the hot path (rgb2hsv, RGB statistics,
+ * HSV-grid colour palette, 2-D FFT magnitude + polar blur binning) runs as
+ * hand-written HIP kernels on a gfx950 GPU; there is no CPU fallback -- without
+ * a usable GPU every entry point returns NULL / a negative status and
+ * phd_last_error() says why.
+ *
+ * Everything here is plain C: pointers, ints and doubles, no HIP/torch types.
+ */
+#ifndef PHOTOHIVE_DSP_H
+#define PHOTOHIVE_DSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- struct layouts: byte-identical to the reference ------------------- */
+typedef double Pixel;                                  /* src/types.h:5 */
+
+typedef struct Pixel_HSV {                             /* src/image_processing.h:12-17 */
+    int parent_id;
+    double h, s, v;
+} Pixel_HSV;
+
+typedef struct Image_RGB {                             /* src/image_processing.h:31-36 */
+    int height, width;
+    Pixel *r, *g, *b;
+} Image_RGB;
+
+typedef struct Image_PGM {                             /* src/image_processing.h:63-66 */
+    int height, width;
+    Pixel* data;
+} Image_PGM;
+
+typedef struct RGB_Statistics {                        /* src/image_processing.h:73-80 */
+    Pixel Br, Bg, Bb, Cr, Cg, Cb;
+} RGB_Statistics;
+
+typedef struct Crop_Boundaries {                       /* src/image_processing.h:92-98 */
+    int N;
+    int *top, *bottom, *left, *right;
+} Crop_Boundaries;
+
+typedef struct Color_Palette {                         /* src/color_quantization.h:11-15 */
+    int N;
+    Pixel_HSV* averages;
+    double* percentages;
+} Color_Palette;
+
+typedef double Bin;                                    /* src/blur_profile.h:8 */
+
+typedef struct Blur_Profile {                          /* src/blur_profile.h:20-24 */
+    int num_angle_bins, num_radius_bins;
+    int angle_bin_size, radius_bin_size;
+    Bin** bins;                                        /* [angle][radius] */
+} Blur_Profile;
+
+typedef struct Blur_Vector {                           /* src/blur_profile.h:52-55 */
+    int angle;
+    float magnitude;
+} Blur_Vector;
+
+typedef struct Blur_Vector_Group {                     /* src/blur_profile.h:58-61 */
+    int len_vectors;
+    Blur_Vector* blur_vectors;
+} Blur_Vector_Group;
+
+typedef struct Sharpnesses {                           /* src/utilities.h:25-28 */
+    int N;
+    Pixel* sharpness;
+} Sharpnesses;
+
+typedef struct Full_Report_Data {                      /* src/utilities.h:30-37 */
+    RGB_Statistics* rgb_stats;
+    Color_Palette* color_palette;
+    Blur_Profile* blur_profile;
+    Blur_Vector_Group* blur_vectors;
+    Pixel average_saturation;
+    Sharpnesses* sharpness;
+} Full_Report_Data;
+
+/* ---- legacy entry points (reference signatures) ------------------------- */
+
+/* Replaces get_full_report_data, src/interface.h:16-23 / src/interface.c:20-94.
+ * Input: planar doubles in [0,1] (as utils.py:30-46 produces).  Inputs that are
+ * exactly k/255.0 take the u8 path; any other doubles are rejected with a
+ * message (round 1).  Returns NULL on the reference's error cases
+ * (src/utilities.c:64-87) and on GPU errors. */
+Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundaries* salient_characters,
+                                       int h_partitions, int s_partitions, int v_partitions,
+                                       double black_thresh, double gray_thresh,
+                                       double coverage_thresh, int linked_list_size,
+                                       int downsample_rate, int radius_partitions,
+                                       int angle_partitions, float quantity_weight,
+                                       float saturation_value_weight, double fft_streak_thresh,
+                                       double magnitude_thresh, int blur_cutoff_ratio_denom);
+
+/* Replaces free_full_report, src/interface.c:97-111: frees the whole tree and
+ * sets *report = NULL. */
+void free_full_report(Full_Report_Data** report);
+
+/* Replaces get_blur_profile_visual, src/blur_profile.c:140-180 (bound by
+ * /root/reference/lib.py:36-37).  Caller owns the result (free with
+ * phd_free_pgm; the reference's Python caller leaks it). */
+Image_PGM* get_blur_profile_visual(Blur_Profile* blur_profile, int height, int width);
+
+/* ---- new entry points ---------------------------------------------------- */
+
+/* The 16 scalar hyper-parameters of get_report (core.py:442-448), reentrant. */
+typedef struct phd_config {
+    int h_partitions, s_partitions, v_partitions;
+    double black_thresh, gray_thresh, coverage_thresh;
+    int linked_list_size, downsample_rate;
+    int radius_partitions, angle_partitions;
+    float quantity_weight, saturation_value_weight;
+    double fft_streak_thresh, magnitude_thresh;
+    int blur_cutoff_ratio_denom;
+} phd_config;
+
+/* Fill *cfg with the get_report defaults (18,2,3,0.1,0.1,0.95,1000,1,40,72,
+ * 0.1f,0.9f,1.20,0.3,2). */
+void phd_config_default(phd_config* cfg);
+
+/* One image from an interleaved RGB8 HOST buffer (row_stride bytes per row;
+ * 0 = 3*width).  No planar-double conversion.  NULL on error. */
+Full_Report_Data* phd_report_u8(const uint8_t* rgb, int height, int width, size_t row_stride,
+                                const phd_config* cfg, const Crop_Boundaries* crops);
+
+/* A batch of same-size images already resident in GPU memory (d_rgb points at
+ * n_images * image_stride bytes on the current HIP device; rows are 3*width
+ * bytes).  stream: a hipStream_t or NULL for the library's own stream.
+ * out[i] receives each report (NULL on per-image error, status[i] < 0).
+ * Returns 0 when every image succeeded, else the number of failures, or -1
+ * on a setup error. */
+int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
+                            size_t image_stride, const phd_config* cfg, Full_Report_Data** out,
+                            int* status, void* stream);
+
+/* A batch of host images of any sizes (config 5 of BASELINE.json). */
+int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
+                        int n_images, const phd_config* cfg, Full_Report_Data** out, int* status);
+
+/* Palette intermediates of one device-resident image, for bit-exact checks:
+ * hist[TL] (arm_octree quantities), parents[*n_parents] (valid_parents in
+ * palette order), kept[*n_parents] (pixels surviving group_irregular_pixels).
+ * Arrays must hold total_length (hist) / total_length (parents, kept) ints.
+ * Returns total_length, or < 0 on error. */
+int phd_palette_trace_device(const uint8_t* d_rgb, int height, int width, const phd_config* cfg,
+                             int* hist, int* parents, int* kept, int* n_parents);
+
+/* Per-bin element counts of the polar blur table for a height x width image
+ * (image-independent, src/blur_profile.c:87-98), [angle][radius] row-major.
+ * Returns 0 or < 0. */
+int phd_blur_counts(int height, int width, int radius_partitions, int angle_partitions,
+                    long long* counts);
+
+/* Fill n bytes of device memory with the splitmix64 stream of
+ * photohive_dsp_amd/synth.py:uniform (byte j = byte j%8 of word j/8). */
+int phd_fill_uniform_device(uint8_t* d_dst, size_t n, uint64_t seed, void* stream);
+
+/* Validation hook: per-pixel rgb2hsv and octree group id of n_pixels device
+ * RGB8 pixels into d_gid[n] (and d_hsv[3n] if non-NULL). */
+int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, const phd_config* cfg, int* d_gid,
+                                double* d_hsv);
+
+/* Free an Image_PGM returned by get_blur_profile_visual. */
+void phd_free_pgm(Image_PGM* img);
+
+/* Human-readable reason for the last failure on this thread ("" if none). */
+const char* phd_last_error(void);
+
+/* Device name / arch / CU count into buf; returns the HIP device ordinal or < 0. */
+int phd_device_info(char* buf, int buflen);
+
+/* Per-stage GPU timing of the most recent call on this thread (ms, from HIP
+ * events on the library stream): [0] hsv+stats, [1] fft rows, [2] fft columns,
+ * [3] palette pass 2, [4] whole call.  Returns the number of stages written. */
+int phd_last_timings(double* ms, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHOTOHIVE_DSP_H */

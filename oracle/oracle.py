@@ -67,6 +67,7 @@ def lib():
         L.orc_vectorize.argtypes = [P(C.c_double), C.c_int, C.c_int, C.c_double, C.c_double,
                                     C.c_int, P(C.c_int), P(C.c_float)]
         L.orc_newton_int_sqrt.argtypes = [C.c_double]
+        L.orc_group_ids.argtypes = [u8p, C.c_long, P(OrcConfig), P(C.c_int), P(C.c_double)]
         L.orc_sharpness.argtypes = [u8p, C.c_int, C.c_int, C.c_int] + [P(C.c_int)] * 4 + [P(C.c_double)]
         _lib = L
     return _lib
@@ -131,6 +132,18 @@ def palette(img, **kw):
     )
     lib().orc_palette_free(C.byref(pal))
     return res
+
+
+def group_ids(rgb: np.ndarray, with_hsv: bool = False, **kw):
+    """HSV group id (and h, s, v) of every pixel of an (..., 3) u8 array."""
+    flat, p = _u8(rgb.reshape(-1, 3))
+    n = flat.shape[0]
+    gid = np.empty(n, dtype=np.int32)
+    hsv = np.empty((n, 3)) if with_hsv else None
+    cfg = make_config(**kw)
+    lib().orc_group_ids(p, n, C.byref(cfg), gid.ctypes.data_as(C.POINTER(C.c_int)),
+                        hsv.ctypes.data_as(C.POINTER(C.c_double)) if with_hsv else None)
+    return (gid, hsv) if with_hsv else gid
 
 
 def power_spectrum(pgm: np.ndarray, workers: int = 1) -> np.ndarray:

@@ -356,6 +356,19 @@ void orc_palette_free(orc_palette* p) {
     memset(p, 0, sizeof(*p));
 }
 
+void orc_group_ids(const uint8_t* rgb, long n, const orc_config* cfg, int* gid, double* hsv) {
+    grid G;
+    grid_init(&G, cfg);
+    for (long i = 0; i < n; i++) {
+        double h, s, v;
+        orc_rgb2hsv_px((double)rgb[3 * i] / 255.0, (double)rgb[3 * i + 1] / 255.0,
+                       (double)rgb[3 * i + 2] / 255.0, &h, &s, &v);
+        gid[i] = group_of(&G, h, s, v);
+        if (hsv) { hsv[3 * i] = h; hsv[3 * i + 1] = s; hsv[3 * i + 2] = v; }
+    }
+    grid_free(&G);
+}
+
 /* ------------------------------------------------------------ luminance */
 void orc_pgm_dc(const uint8_t* rgb, int height, int width, double avg, double* out) {
     long n = (long)height * width;

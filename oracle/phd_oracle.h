@@ -55,6 +55,10 @@ int orc_palette_run(const uint8_t* rgb, int height, int width, const orc_config*
                     orc_palette* out);
 void orc_palette_free(orc_palette* p);
 
+/* Per-pixel HSV (image_processing.c:384-415) and arm_octree group id
+   (color_quantization.c:131-145) of n interleaved u8 pixels. */
+void orc_group_ids(const uint8_t* rgb, long n, const orc_config* cfg, int* gid, double* hsv);
+
 /* rgb2pgm (image_processing.c:505-512) followed by remove_dc_bias
    (blur_profile.c:233-238): out[i] = (0.299r+0.587g+0.114b) - avg. */
 void orc_pgm_dc(const uint8_t* rgb, int height, int width, double avg, double* out);

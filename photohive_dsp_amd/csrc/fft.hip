@@ -1,0 +1,333 @@
+// fft.hip -- 2-D real FFT power spectrum fused with the polar blur binning.
+//
+// Replaces pgm_fft + pgm_normalize_fft (src/fft_processing.c:18-63, 173-213; the
+// DFT itself is FFTW3 r2c, unnormalised, e^{-i}), rgb2pgm + remove_dc_bias
+// (src/image_processing.c:505-512, src/blur_profile.c:233-238) and the binning
+// loop of calculate_blur_profile (src/blur_profile.c:87-100).
+//
+//  * Row pass: one block per PAIR of image rows.  Luma - avg of row y0 (real)
+//    and row y0+1 (imaginary) is built straight from the RGB8 bytes, one
+//    complex FFT of length W runs in LDS, and the two half spectra
+//    (W/2+1 bins each) are separated and written row-major to `inter`.
+//  * Column pass: one block per C adjacent spectrum columns; C length-H FFTs
+//    in LDS, then the epilogue forms p = re*re + im*im, keeps a running max and
+//    accumulates log(p) for p >= 1 into the element's polar bin (LDS), so the
+//    normalised spectrum is never written: G_s = 1/(2 log(sqrt(max)+1)) is a
+//    common factor applied on the host ( sum(log p * G_s) = G_s * sum(log p) ).
+//
+// FFT engine: in-place Stockham autosort in LDS, every pass = all threads read
+// their butterflies' inputs into registers, barrier, write.  Twiddles come
+// from a host-built table tw[t] = exp(-2 pi i t/n) (long-double accurate).
+#include "phd_device.h"
+
+namespace phd {
+
+constexpr int kFftThreads = 512;
+
+namespace {
+
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 mul_negi(double2 a) { return make_double2(a.y, -a.x); }   // a * (-i)
+__device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
+
+template <int R>
+__device__ __forceinline__ void butterfly(double2 (&v)[R]);
+
+template <>
+__device__ __forceinline__ void butterfly<2>(double2 (&v)[2]) {
+    const double2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+}
+
+template <>
+__device__ __forceinline__ void butterfly<3>(double2 (&v)[3]) {
+    constexpr double s1 = 0.86602540378443864676;   // sin(2 pi / 3)
+    const double2 t = cadd(v[1], v[2]);
+    const double2 d = mul_negi(cscale(csub(v[1], v[2]), s1));   // -i s1 (v1 - v2)
+    const double2 m = make_double2(v[0].x - 0.5 * t.x, v[0].y - 0.5 * t.y);
+    v[0] = cadd(v[0], t);
+    v[1] = cadd(m, d);
+    v[2] = csub(m, d);
+}
+
+template <>
+__device__ __forceinline__ void butterfly<4>(double2 (&v)[4]) {
+    const double2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    const double2 t2 = cadd(v[1], v[3]), t3 = mul_negi(csub(v[1], v[3]));
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+}
+
+template <>
+__device__ __forceinline__ void butterfly<5>(double2 (&v)[5]) {
+    constexpr double c1 = 0.30901699437494742410;    // cos(2 pi / 5)
+    constexpr double c2 = -0.80901699437494742410;   // cos(4 pi / 5)
+    constexpr double s1 = 0.95105651629515357212;    // sin(2 pi / 5)
+    constexpr double s2 = 0.58778525229247312917;    // sin(4 pi / 5)
+    const double2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
+    const double2 t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
+    const double2 a1 = make_double2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
+    const double2 a2 = make_double2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
+    const double2 b1 = mul_negi(make_double2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y));
+    const double2 b2 = mul_negi(make_double2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y));
+    v[0] = cadd(v[0], cadd(t1, t2));
+    v[1] = cadd(a1, b1);
+    v[4] = csub(a1, b1);
+    v[2] = cadd(a2, b2);
+    v[3] = csub(a2, b2);
+}
+
+template <>
+__device__ __forceinline__ void butterfly<8>(double2 (&v)[8]) {
+    constexpr double h = 0.70710678118654752440;   // sqrt(1/2)
+    double2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+    butterfly<4>(e);
+    butterfly<4>(o);
+    // o[k] *= W8^k
+    o[1] = make_double2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
+    o[2] = mul_negi(o[2]);
+    o[3] = make_double2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        v[k] = cadd(e[k], o[k]);
+        v[k + 4] = csub(e[k], o[k]);
+    }
+}
+
+// One Stockham pass of radix R over `nseq` sequences of length n stored at
+// buf + seq*n (Govindaraju et al. formulation: read stride n/R, write
+// expanded index (j/Ns)*Ns*R + j%Ns + r*Ns).
+template <int R>
+__device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns, const double2* __restrict__ tw) {
+    constexpr int NB = (kFftMaxLds + R * kFftThreads - 1) / (R * kFftThreads);
+    const int nb = n / R, total = nb * nseq, tstep = n / (Ns * R);
+    double2 v[NB][R];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const int t = threadIdx.x + b * kFftThreads;
+        if (t < total) {
+            const int seq = t / nb, j = t - seq * nb;
+            const double2* s = buf + seq * n;
+#pragma unroll
+            for (int r = 0; r < R; r++) v[b][r] = s[j + r * nb];
+            const int jm = j % Ns;
+            if (jm != 0) {
+#pragma unroll
+                for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * tstep]);
+            }
+            butterfly<R>(v[b]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        const int t = threadIdx.x + b * kFftThreads;
+        if (t < total) {
+            const int seq = t / nb, j = t - seq * nb;
+            double2* s = buf + seq * n;
+            const int jm = j % Ns;
+            const int d = (j / Ns) * Ns * R + jm;
+#pragma unroll
+            for (int r = 0; r < R; r++) s[d + r * Ns] = v[b][r];
+        }
+    }
+    __syncthreads();
+}
+
+// Generic radix (any R, incl. a prime length itself): output-parallel direct DFT.
+__device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns, int R, const double2* __restrict__ tw) {
+    constexpr int EG = kFftMaxLds / kFftThreads;   // outputs per thread (nseq*n <= kFftMaxLds)
+    const int nb = n / R, total = n * nseq, tstep = n / (Ns * R), nr = n / R;
+    double2 out[EG];
+#pragma unroll
+    for (int e = 0; e < EG; e++) {
+        const int t = threadIdx.x + e * kFftThreads;
+        if (t < total) {
+            const int seq = t / n, rem = t - seq * n;
+            const int j = rem / R, k = rem - j * R;       // butterfly j, output k
+            const double2* s = buf + seq * n;
+            const int jm = j % Ns;
+            const int step = jm * tstep + k * nr;         // twiddle exponent per input r (mod n)
+            double2 acc = make_double2(0.0, 0.0);
+            int ex = 0;
+            for (int r = 0; r < R; r++) {
+                acc = cadd(acc, cmul(s[j + r * nb], tw[ex]));
+                ex += step;
+                if (ex >= n) ex -= n * (ex / n);
+            }
+            out[e] = acc;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EG; e++) {
+        const int t = threadIdx.x + e * kFftThreads;
+        if (t < total) {
+            const int seq = t / n, rem = t - seq * n;
+            const int j = rem / R, k = rem - j * R;
+            const int jm = j % Ns;
+            buf[seq * n + (j / Ns) * Ns * R + jm + k * Ns] = out[e];
+        }
+    }
+    __syncthreads();
+}
+
+__device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan) {
+    int Ns = 1;
+    for (int p = 0; p < plan.npass; p++) {
+        const int R = plan.radix[p];
+        switch (R) {
+            case 2: stockham_pass<2>(buf, plan.n, nseq, Ns, plan.tw); break;
+            case 3: stockham_pass<3>(buf, plan.n, nseq, Ns, plan.tw); break;
+            case 4: stockham_pass<4>(buf, plan.n, nseq, Ns, plan.tw); break;
+            case 5: stockham_pass<5>(buf, plan.n, nseq, Ns, plan.tw); break;
+            case 8: stockham_pass<8>(buf, plan.n, nseq, Ns, plan.tw); break;
+            default: generic_pass(buf, plan.n, nseq, Ns, R, plan.tw); break;
+        }
+        Ns *= R;
+    }
+}
+
+__global__ __launch_bounds__(kFftThreads) void k_fft_rows(const uint8_t* __restrict__ img, int H, int W,
+                                                          FftPlan plan,
+                                                          const unsigned long long* __restrict__ sums,
+                                                          const double* __restrict__ k255g,
+                                                          double2* __restrict__ inter) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double2* buf = reinterpret_cast<double2*>(smem);
+    double* k255 = reinterpret_cast<double*>(smem + sizeof(double2) * W);
+    const int tid = threadIdx.x;
+    if (tid < 256) k255[tid] = k255g[tid];
+    // avg = (Br + Bg + Bb) / 3 (src/interface.c:78) from the exact integer sums
+    const double n = (double)H * (double)W;
+    const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
+                        (double)sums[2] / 255.0 / n) / 3.0;
+    __syncthreads();
+    const int y0 = 2 * blockIdx.x, y1 = y0 + 1;
+    const bool two = y1 < H;
+    const uint8_t* r0 = img + (size_t)y0 * W * 3;
+    const uint8_t* r1 = img + (size_t)(two ? y1 : y0) * W * 3;
+    for (int x = tid; x < W; x += kFftThreads) {
+        // rgb2pgm (image_processing.c:509), then remove_dc_bias (blur_profile.c:236)
+        const double p0 = 0.299 * k255[r0[3 * x]] + 0.587 * k255[r0[3 * x + 1]] + 0.114 * k255[r0[3 * x + 2]];
+        const double p1 = 0.299 * k255[r1[3 * x]] + 0.587 * k255[r1[3 * x + 1]] + 0.114 * k255[r1[3 * x + 2]];
+        buf[x] = make_double2(p0 - avg, two ? p1 - avg : 0.0);
+    }
+    __syncthreads();
+    fft_lds(buf, 1, plan);
+    // Z = A + iB with A, B the spectra of the two real rows:
+    // A[k] = (Z[k] + conj Z[W-k]) / 2, B[k] = (Z[k] - conj Z[W-k]) / (2i)
+    const int wf = W / 2 + 1;
+    double2* o0 = inter + (size_t)y0 * wf;
+    double2* o1 = inter + (size_t)y1 * wf;
+    for (int k = tid; k < wf; k += kFftThreads) {
+        const double2 zk = buf[k], zm = buf[k == 0 ? 0 : W - k];
+        o0[k] = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+        if (two) o1[k] = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+    }
+}
+
+__global__ __launch_bounds__(kFftThreads) void k_fft_cols(const double2* __restrict__ inter, int H, int wf,
+                                                          int C, FftPlan plan,
+                                                          const uint16_t* __restrict__ binmap, int nbins,
+                                                          int lds_bins, double* __restrict__ bin_sums,
+                                                          unsigned long long* __restrict__ fmax_bits) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double2* buf = reinterpret_cast<double2*>(smem);
+    const int tid = threadIdx.x;
+    const int k0 = blockIdx.x * C;
+    const int nc = min(C, wf - k0);
+    double* lb = reinterpret_cast<double*>(smem + sizeof(double2) * (size_t)C * H);
+    if (lds_bins)
+        for (int i = tid; i < nbins; i += kFftThreads) lb[i] = 0.0;
+    for (int i = tid; i < nc * H; i += kFftThreads) {
+        const int y = i / nc, c = i - y * nc;
+        buf[c * H + y] = inter[(size_t)y * wf + k0 + c];
+    }
+    __syncthreads();
+    fft_lds(buf, nc, plan);
+    double mx = 0.0;
+    double* acc = lds_bins ? lb : bin_sums;
+    const int total = nc * H;
+    for (int i0 = 0; i0 < total; i0 += kFftThreads) {
+        const int i = i0 + tid;
+        int b = -1;
+        double lg = 0.0;
+        if (i < total) {
+            const double2 X = buf[i];
+            const double p = X.x * X.x + X.y * X.y;      // fft_processing.c:49
+            mx = fmax(mx, p);
+            if (p >= 1) {                               // fft_processing.c:197-198
+                const int c = i / H, u = i - c * H;
+                b = binmap[(size_t)(k0 + c) * H + u];
+                lg = log(p);
+            }
+        }
+        const int b0 = __builtin_amdgcn_readfirstlane(b);
+        if (__all(b == b0)) {
+            const double t = wave_sum(lg);
+            if (b0 >= 0 && lane_id() == 0) atomicAdd(&acc[b0], t);
+        } else if (b >= 0) {
+            atomicAdd(&acc[b], lg);
+        }
+    }
+    mx = wave_max(mx);
+    if (lane_id() == 0) atomicMax(fmax_bits, (unsigned long long)__double_as_longlong(mx));
+    if (lds_bins) {
+        __syncthreads();
+        for (int i = tid; i < nbins; i += kFftThreads) {
+            const double a = lb[i];
+            if (a != 0.0) atomicAdd(&bin_sums[i], a);
+        }
+    }
+}
+
+}  // namespace
+
+// Kernels here may use up to the full 160 KiB LDS of a gfx950 CU.
+static void allow_big_lds() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fft_rows),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fft_cols),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftPlan& plan,
+                           const unsigned long long* sums, const double* k255, double2* inter,
+                           hipStream_t st) {
+    allow_big_lds();
+    const size_t lds = sizeof(double2) * width + 256 * sizeof(double);
+    hipLaunchKernelGGL(k_fft_rows, dim3((height + 1) / 2), dim3(kFftThreads), lds, st, img, height,
+                       width, plan, sums, k255, inter);
+    return hipGetLastError();
+}
+
+hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
+                           const uint16_t* binmap, int nbins, double* bin_sums,
+                           unsigned long long* fmax_bits, hipStream_t st) {
+    allow_big_lds();
+    constexpr size_t kLdsBudget = 152 * 1024;
+    const size_t bins_bytes = sizeof(double) * nbins;
+    const int lds_bins = bins_bytes <= 48 * 1024;
+    const size_t col_bytes = sizeof(double2) * height;
+    int C = 1;
+    while (C < 8 && (size_t)(2 * C) * height <= (size_t)kFftMaxLds &&
+           (2 * C) * col_bytes + (lds_bins ? bins_bytes : 0) <= kLdsBudget)
+        C *= 2;
+    const size_t lds = C * col_bytes + (lds_bins ? bins_bytes : 0);
+    hipLaunchKernelGGL(k_fft_cols, dim3((wf + C - 1) / C), dim3(kFftThreads), lds, st, inter, height,
+                       wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_bits);
+    return hipGetLastError();
+}
+
+}  // namespace phd

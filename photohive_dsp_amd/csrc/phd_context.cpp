@@ -1,0 +1,178 @@
+// phd_context.cpp -- per-device state: stream, constant tables, FFT plans,
+// polar bin tables and grow-only workspaces.  One context per HIP device; a
+// mutex serialises calls that share it (the API itself keeps no globals per
+// call, unlike the reference's QUANTITY_WEIGHT / num_cores / FFTW state).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "phd_host.h"
+
+namespace phd {
+
+namespace {
+thread_local std::string g_error;
+thread_local double g_timings[8];
+thread_local int g_ntimings = 0;
+std::mutex g_ctx_mu;
+Context* g_ctx[64] = {};
+}  // namespace
+
+void set_error(const std::string& msg) {
+    g_error = msg;
+    if (!getenv("PHD_QUIET")) fprintf(stderr, "photohive_dsp_amd: %s\n", msg.c_str());
+}
+void clear_error() { g_error.clear(); }
+
+void record_timings(const double* ms, int n) {
+    g_ntimings = n < 8 ? n : 8;
+    for (int i = 0; i < g_ntimings; i++) g_timings[i] = ms[i];
+}
+
+Context* get_context() {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+            set_error("no HIP device available: the MI355X path has no CPU fallback");
+            return nullptr;
+        }
+        dev = 0;
+        if (hipSetDevice(0) != hipSuccess) {
+            set_error("hipSetDevice(0) failed");
+            return nullptr;
+        }
+    }
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    if (g_ctx[dev]) return g_ctx[dev];
+    auto* c = new Context();
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("hipStreamCreate failed");
+        delete c;
+        return nullptr;
+    }
+    double k255[256];
+    for (int k = 0; k < 256; k++) k255[k] = (double)k / 255.0;   // utils.py:30-46 (== C's k/255.0)
+    if (hipMalloc(&c->d_k255, sizeof(k255)) != hipSuccess ||
+        hipMemcpy(c->d_k255, k255, sizeof(k255), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("device table upload failed");
+        delete c;
+        return nullptr;
+    }
+    for (auto& e : c->ev) (void)hipEventCreate(&e);
+    g_ctx[dev] = c;
+    return c;
+}
+
+bool ensure_device(void** p, size_t* cap, size_t need) {
+    if (*cap >= need && *p) return true;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    size_t sz = need + need / 4 + 4096;
+    if (hipMalloc(p, sz) != hipSuccess) {
+        set_error("hipMalloc of " + std::to_string(sz) + " bytes failed");
+        *p = nullptr;
+        return false;
+    }
+    *cap = sz;
+    return true;
+}
+
+bool ensure_pinned(Context* c, size_t need) {
+    if (c->pin_bytes >= need && c->h_pin) return true;
+    if (c->h_pin) (void)hipHostFree(c->h_pin);
+    c->h_pin = nullptr;
+    size_t sz = need + need / 4 + 4096;
+    if (hipHostMalloc(&c->h_pin, sz, hipHostMallocDefault) != hipSuccess) {
+        set_error("hipHostMalloc failed");
+        c->pin_bytes = 0;
+        return false;
+    }
+    c->pin_bytes = sz;
+    return true;
+}
+
+// ---- FFT plans ---------------------------------------------------------------
+bool make_fft_plan(int n, FftPlanHost* p) {
+    if (n < 1 || n > kFftMaxLds) {
+        set_error("FFT length " + std::to_string(n) + " exceeds the LDS-resident limit " +
+                  std::to_string(kFftMaxLds) + " of this build");
+        return false;
+    }
+    FftPlan& P = p->plan;
+    P.n = n;
+    P.npass = 0;
+    int m = n;
+    // radix order: 8s, then 4, then 2, 5, 3, then any remaining prime factor
+    while (m % 8 == 0 && P.npass < kMaxFftPasses) { P.radix[P.npass++] = 8; m /= 8; }
+    if (m % 4 == 0) { P.radix[P.npass++] = 4; m /= 4; }
+    if (m % 2 == 0) { P.radix[P.npass++] = 2; m /= 2; }
+    while (m % 5 == 0 && P.npass < kMaxFftPasses) { P.radix[P.npass++] = 5; m /= 5; }
+    while (m % 3 == 0 && P.npass < kMaxFftPasses) { P.radix[P.npass++] = 3; m /= 3; }
+    for (int f = 7; m > 1 && P.npass < kMaxFftPasses;) {
+        if ((long)f * f > m) { P.radix[P.npass++] = m; m = 1; break; }
+        if (m % f == 0) { P.radix[P.npass++] = f; m /= f; }
+        else f += 2;
+    }
+    if (m != 1) {
+        set_error("FFT length " + std::to_string(n) + " has too many factors");
+        return false;
+    }
+    std::vector<double2> tw(n);
+    const long double two_pi = 6.283185307179586476925286766559005768L;
+    for (int t = 0; t < n; t++) {
+        const long double a = two_pi * (long double)t / (long double)n;
+        tw[t] = make_double2((double)cosl(a), (double)-sinl(a));
+    }
+    if (hipMalloc(&p->d_tw, sizeof(double2) * n) != hipSuccess ||
+        hipMemcpy(p->d_tw, tw.data(), sizeof(double2) * n, hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("twiddle upload failed");
+        return false;
+    }
+    P.tw = p->d_tw;
+    return true;
+}
+
+const FftPlanHost* get_plan(Context* c, int n) {
+    auto it = c->plans.find(n);
+    if (it != c->plans.end()) return &it->second;
+    FftPlanHost p;
+    if (!make_fft_plan(n, &p)) return nullptr;
+    return &(c->plans[n] = p);
+}
+
+const BlurTable* get_table(Context* c, int height, int width, int nr, int na) {
+    auto key = std::make_tuple(height, width, nr, na);
+    auto it = c->tables.find(key);
+    if (it != c->tables.end()) return &it->second;
+    BlurTable t;
+    if (!build_blur_table(height, width, nr, na, &t)) return nullptr;
+    return &(c->tables[key] = std::move(t));
+}
+
+}  // namespace phd
+
+extern "C" const char* phd_last_error(void) { return phd::g_error.c_str(); }
+
+extern "C" int phd_last_timings(double* ms, int n) {
+    int k = n < phd::g_ntimings ? n : phd::g_ntimings;
+    for (int i = 0; i < k; i++) ms[i] = phd::g_timings[i];
+    return k;
+}
+
+extern "C" int phd_device_info(char* buf, int buflen) {
+    int dev = -1, n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        if (buf && buflen > 0) snprintf(buf, buflen, "no HIP device");
+        return -1;
+    }
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return -1;
+    if (buf && buflen > 0)
+        snprintf(buf, buflen, "%s %s CUs=%d HBM=%.1fGB", pr.name, pr.gcnArchName, pr.multiProcessorCount,
+                 pr.totalGlobalMem / 1e9);
+    return dev;
+}

@@ -1,0 +1,114 @@
+// phd_host.h -- host-side internals of libreport_data.so (C++17).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/photohive_dsp.h"
+#include "phd_internal.h"
+
+namespace phd {
+
+// ---- errors ---------------------------------------------------------------
+void set_error(const std::string& msg);   // thread-local, also printed to stderr
+void clear_error();
+
+#define PHD_HIP(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            ::phd::set_error(std::string("HIP error ") + hipGetErrorString(e_) + " at " \
+                             + __FILE__ + ":" + std::to_string(__LINE__) + " (" #expr ")"); \
+            return false;                                                               \
+        }                                                                               \
+    } while (0)
+
+// ---- validated configuration ----------------------------------------------
+// Returns false (with phd_last_error) for configurations where the reference's
+// behaviour is undefined (see DESIGN.md "Deliberate rejections").
+bool validate_config(const phd_config& cfg, std::string* why);
+GridParams make_grid(const phd_config& cfg);
+// Group centres of initialize_octree (src/color_quantization.c:57-99).
+struct GroupCenters {
+    std::vector<double> h, s, v;
+};
+GroupCenters make_centers(const GridParams& gp);
+
+// ---- palette decisions (host) ---------------------------------------------
+struct PaletteDecision {
+    std::vector<int> parents;            // valid_parents, palette order
+    std::vector<GroupRule> rules;        // [TL]
+    std::vector<long long> kept;         // pixels each parent keeps
+    std::vector<double> off;             // 180 - h_centre(parent)
+    std::vector<int> search;             // groups needing the device cutoff search
+};
+// find_valid_octree_parents + group_irregular_pixels as keep rules.
+bool decide_palette(const GridParams& gp, const GroupCenters& gc, const unsigned* hist, long n_hsv,
+                    const phd_config& cfg, PaletteDecision* out);
+
+// ---- blur profile helpers (host) ------------------------------------------
+struct BlurTable {
+    int height = 0, wf = 0, nr = 0, na = 0;
+    std::vector<long long> counts;       // [na*nr]
+    uint16_t* d_map = nullptr;           // device [wf][height]
+    int angle_bin_size = 0, radius_bin_size = 0;
+};
+// Exact (phi_bin, r_bin) of every spectrum element, glibc atan2 + newton_int_sqrt
+// exactly as src/blur_profile.c:87-97 / 427-458.
+bool build_blur_table(int height, int width, int nr, int na, BlurTable* t);
+void vectorize_blur(const double* bins, int na, int nr, double streak, double mag, int denom,
+                    Blur_Vector* out10);
+
+// ---- FFT plans --------------------------------------------------------------
+struct FftPlanHost {
+    FftPlan plan{};
+    double2* d_tw = nullptr;
+};
+bool make_fft_plan(int n, FftPlanHost* p);
+
+// ---- device context ---------------------------------------------------------
+struct Context {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    double* d_k255 = nullptr;                       // k/255.0 for k in [0,256)
+    std::map<int, FftPlanHost> plans;
+    std::map<std::tuple<int, int, int, int>, BlurTable> tables;
+    // grow-only workspaces
+    void* d_ws = nullptr;
+    size_t ws_bytes = 0;
+    void* h_pin = nullptr;
+    size_t pin_bytes = 0;
+    double2* d_inter = nullptr;
+    size_t inter_bytes = 0;
+    uint8_t* d_stage = nullptr;                    // upload staging for host images
+    size_t stage_bytes = 0;
+    hipEvent_t ev[8] = {};
+    std::mutex mu;
+};
+// The context of the current HIP device (created on first use).  nullptr if no GPU.
+Context* get_context();
+bool ensure_device(void** p, size_t* cap, size_t need);
+bool ensure_pinned(Context* c, size_t need);
+const FftPlanHost* get_plan(Context* c, int n);
+const BlurTable* get_table(Context* c, int height, int width, int nr, int na);
+
+// ---- the pipeline -----------------------------------------------------------
+struct ImageIn {
+    const uint8_t* d_img;   // device RGB8, rows of 3*width bytes
+};
+// Run the full report on n same-size device images.  out[i]/status[i] per image.
+bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, int width,
+                 const phd_config& cfg, const Crop_Boundaries* crops, Full_Report_Data** out,
+                 int* status, hipStream_t stream);
+// Palette intermediates only (for parity tests).
+bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, const phd_config& cfg,
+                       std::vector<unsigned>* hist, PaletteDecision* dec,
+                       std::vector<double>* device_counts);
+
+void record_timings(const double* ms, int n);
+
+}  // namespace phd

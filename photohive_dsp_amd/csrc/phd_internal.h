@@ -1,0 +1,87 @@
+// phd_internal.h -- shared between the host C++ (phd_*.cpp) and the HIP kernels
+// (*.hip).  Plain POD types and launcher declarations only.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace phd {
+
+// Pixels per palette chunk: the unit of work of the hsv/stats kernel and the
+// palette-sums kernel, and the granularity of the per-chunk group histograms
+// the tie-overflow cutoff search walks (counts fit uint16).
+constexpr int kChunk = 16384;
+constexpr int kThreads = 256;
+// Largest FFT length kept resident in LDS (complex fp64, 16 B/element).
+constexpr int kFftMaxLds = 8192;
+constexpr int kMaxFftPasses = 24;
+
+// The HSV grid of initialize_octree (src/color_quantization.c:22-101).
+struct GridParams {
+    int hp, sp, vp, ng, tl;
+    double Lh, Ls, Lv, bt, gt;
+};
+
+// Per-image device workspace views used by the palette kernels.
+struct PaletteDev {
+    unsigned long long* sums;     // [6] sum k_r, k_g, k_b, k_r^2, k_g^2, k_b^2 (full image)
+    double* s_part;               // [nchunks] per-chunk sum of HSV saturation
+    unsigned* hist;               // [TL] group quantities
+    unsigned short* chunk_hist;   // [nchunks][TL]
+};
+
+// Keep rule of one octree group after group_irregular_pixels.
+struct GroupRule {
+    int slot;            // palette slot (index into valid_parents) or -1 = dropped
+    int partial;         // 0: every pixel kept; 1: first `keep` pixels (+ last if dangle)
+    int keep;            // pixels kept in raster order (partial only)
+    int dangle;          // the group's last pixel survives as a dangling node
+    unsigned cutoff;     // raster index bound: kept iff idx < cutoff (filled on device)
+    unsigned last;       // raster index of the group's last pixel (filled on device)
+};
+
+// A mixed-radix FFT plan for one length (radix sequence + twiddle table).
+struct FftPlan {
+    int n;
+    int npass;
+    int radix[kMaxFftPasses];
+    const double2* tw;   // device: tw[t] = exp(-2 pi i t / n), t in [0, n)
+};
+
+// ---- launchers (kernels in *.hip) ------------------------------------------
+// hsv/stats/histogram pass over one image (K1).  ds = downsample rate.
+hipError_t launch_hsv_stats(const uint8_t* img, int height, int width, int ds,
+                            const GridParams& gp, const PaletteDev& out, int nchunks,
+                            const double* k255, hipStream_t st);
+// Locate the keep cutoff / last pixel for groups with rule.partial (Kcut).
+hipError_t launch_palette_cutoffs(const uint8_t* img, int height, int width, int ds,
+                                  const GridParams& gp, const unsigned short* chunk_hist,
+                                  int nchunks, GroupRule* rules, const int* search_groups,
+                                  int n_search, const double* k255, hipStream_t st);
+// Per-slot sums over kept pixels (K3): out[slot*4 + {0,1,2,3}] = sum wrap(h+off), s, v, n.
+hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds,
+                               const GridParams& gp, const GroupRule* rules,
+                               const double* slot_off, int nslots, double* out,
+                               const double* k255, hipStream_t st);
+// Row pass: luma - avg of two rows as one complex sequence, FFT, split, write
+// the half spectra row-major into inter[height][wf].
+hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftPlan& plan,
+                           const unsigned long long* sums, const double* k255,
+                           double2* inter, hipStream_t st);
+// Column pass + epilogue: power, running max, sum log(p) over p >= 1 per
+// polar bin (binmap[wf][height], uint16 bin ids).  Accumulates into
+// bin_sums[na*nr] (fp64) and fmax_bits (max power as uint64 bits).
+hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
+                           const uint16_t* binmap, int nbins, double* bin_sums,
+                           unsigned long long* fmax_bits, hipStream_t st);
+hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const double* k255, int* gid,
+                            double* hsv, hipStream_t st);
+hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st);
+// Laplacian-variance sharpness of n crop boxes: sums[2k] = sum f, sums[2k+1] =
+// sum (f - mean)^2 (sums zeroed by the caller).
+hipError_t launch_sharpness(const uint8_t* img, int height, int width, int n, const int* top,
+                            const int* bottom, const int* left, const int* right, const double* k255,
+                            double* sums, hipStream_t st);
+
+}  // namespace phd

@@ -1,0 +1,211 @@
+// phd_palette.cpp -- the palette's decision logic, run on the host between the
+// two device passes (K1 histogram -> decisions -> Kcut/K3 sums).
+//
+// It reproduces, on the TL-sized group histogram alone, what the reference's
+// get_color_palette does with its per-pixel linked lists
+// (src/color_quantization.c:652-684):
+//  * find_valid_octree_parents (:174-203): stable insertion sort
+//    (custom_sort, src/utilities.c:132-153) by the float32 saliency
+//    (:588-595) through compare_quantities (:601-611), whose `(int)` of the
+//    float difference is x86 cvttss2si -> INT_MIN for |d| >= 2^31 or NaN;
+//  * group_irregular_pixels (:342-479) as per-group keep rules: a group with one
+//    nearest parent is spliced whole; a tie sends every pixel to the FIRST tied
+//    parent (get_distance_pixel_to_parent has no return statement; at -O0 it
+//    returns the pixel pointer's bits, identical for all candidates), appended
+//    through the parent's stale tail pointer: the pixels that fit the tail node
+//    survive, and on overflow only the group's last pixel survives as a
+//    dangling node until the next event on that parent replaces it.
+#include <cmath>
+#include <climits>
+#include <cstring>
+
+#include "phd_host.h"
+
+namespace phd {
+
+bool validate_config(const phd_config& c, std::string* why) {
+    auto fail = [&](const char* m) { *why = m; return false; };
+    if (c.h_partitions <= 0 || c.s_partitions <= 0 || c.v_partitions <= 0)
+        return fail("h/s/v_partitions must be positive (initialize_octree, color_quantization.c:28)");
+    if (360 % c.h_partitions != 0)
+        return fail("h_partitions must divide 360: otherwise arm_octree indexes past the hue grid "
+                    "(color_quantization.c:41,143; undefined behaviour in the reference)");
+    if (!(c.black_thresh >= 0 && c.black_thresh < 1) || !(c.gray_thresh >= 0 && c.gray_thresh < 1))
+        return fail("black_thresh and gray_thresh must lie in [0, 1)");
+    if (!(c.coverage_thresh <= 1.0))
+        return fail("coverage_thresh must be <= 1 (find_valid_octree_parents never terminates "
+                    "otherwise, color_quantization.c:202)");
+    if (c.linked_list_size <= 0) return fail("linked_list_size must be positive");
+    if (c.radius_partitions <= 0 || c.angle_partitions <= 0)
+        return fail("radius/angle_partitions must be positive");
+    if ((long)c.radius_partitions * c.angle_partitions > 65535)
+        return fail("radius_partitions * angle_partitions must be <= 65535");
+    if (c.blur_cutoff_ratio_denom <= 0) return fail("blur_cutoff_ratio_denom must be positive");
+    long tl = (long)c.h_partitions * c.s_partitions * c.v_partitions + c.v_partitions + 1;
+    if (tl > 4096) return fail("h*s*v + v + 1 must be <= 4096 groups");
+    return true;
+}
+
+GridParams make_grid(const phd_config& c) {
+    GridParams g{};
+    g.hp = c.h_partitions;
+    g.sp = c.s_partitions;
+    g.vp = c.v_partitions;
+    g.ng = c.v_partitions;                              // num_grays = v_parts, :27
+    g.tl = g.hp * g.sp * g.vp + g.ng + 1;
+    g.Lh = 360 / g.hp;                                  // integer division, :41
+    g.Ls = (1 - c.gray_thresh) / g.sp;
+    g.Lv = (1 - c.black_thresh) / g.vp;
+    g.bt = c.black_thresh;
+    g.gt = c.gray_thresh;
+    return g;
+}
+
+GroupCenters make_centers(const GridParams& g) {
+    GroupCenters gc;
+    gc.h.assign(g.tl, 0.0);
+    gc.s.assign(g.tl, 0.0);
+    gc.v.assign(g.tl, 0.0);
+    const double half_h = g.Lh / 2, s_offs = g.Ls / 2 + g.gt, v_offs = g.Lv / 2 + g.bt;
+    for (int h = 0; h < g.hp; h++)
+        for (int s = 0; s < g.sp; s++)
+            for (int v = 0; v < g.vp; v++) {
+                const int i = h * g.sp * g.vp + s * g.vp + v;
+                gc.h[i] = h * g.Lh + half_h;
+                gc.s[i] = s * g.Ls + s_offs;
+                gc.v[i] = v * g.Lv + v_offs;
+            }
+    const double l_gray = (1.0f - g.bt) / (double)g.ng;  // :78 (1.0f promotes exactly)
+    for (int j = 0; j < g.ng; j++) gc.v[g.hp * g.sp * g.vp + j] = l_gray * j + v_offs;
+    return gc;                                            // black group stays (0, 0, 0)
+}
+
+namespace {
+
+float saliency(unsigned q, double s, double v, float qw, float svw) {
+    const float s_v = (float)(s * v);
+    const float sal = (float)(int)q * (qw + svw * s_v);
+    return sal * 1000;
+}
+
+// compare_quantities' (int)(sal_b - sal_a), as the x86 conversion behaves.
+int compare(float sal_a, float sal_b) {
+    const float d = sal_b - sal_a;
+    if (!(d > -2147483648.0f && d < 2147483648.0f)) return INT_MIN;
+    return (int)d;
+}
+
+double node_distance(const GridParams& g, const GroupCenters& c, int gi, int pi) {
+    const int gray_start = g.tl - (g.ng + 1), black = g.tl - 1;
+    if (gi < gray_start && pi < gray_start) {
+        double hd = std::fabs(c.h[gi] - c.h[pi]);
+        if (hd > 180) hd = 360 - hd;
+        hd *= (1.0) / (360.0);
+        const double sd = c.s[gi] - c.s[pi], vd = c.v[gi] - c.v[pi];
+        return hd * hd + sd * sd + vd * vd;
+    }
+    const bool gray_i = gray_start <= gi && gi < black, gray_p = gray_start <= pi && pi < black;
+    if ((gray_i && pi < gray_start) || (gray_p && gi < gray_start)) {
+        const double sd = c.s[gi] - c.s[pi], vd = c.v[gi] - c.v[pi];
+        return sd * sd + vd * vd;
+    }
+    const double vd = c.v[gi] - c.v[pi];
+    return vd * vd;
+}
+
+}  // namespace
+
+bool decide_palette(const GridParams& g, const GroupCenters& gc, const unsigned* hist, long n_hsv,
+                    const phd_config& cfg, PaletteDecision* out) {
+    const int tl = g.tl;
+    const int L = cfg.linked_list_size;
+    // ---- ordering by saliency (insertion sort, swap while compare < 0)
+    std::vector<float> sal(tl);
+    for (int i = 0; i < tl; i++)
+        sal[i] = saliency(hist[i], gc.s[i], gc.v[i], cfg.quantity_weight, cfg.saturation_value_weight);
+    std::vector<int> order(tl);
+    for (int i = 0; i < tl; i++) order[i] = i;
+    for (int i = 1; i < tl; i++)
+        for (int j = i; j > 0 && compare(sal[order[j]], sal[order[j - 1]]) < 0; j--)
+            std::swap(order[j], order[j - 1]);
+    int goal = (int)((double)n_hsv * cfg.coverage_thresh);
+    int np = -1;
+    for (int i = 0; i < tl; i++) {
+        goal -= (int)hist[order[i]];
+        if (goal <= 0) {
+            np = i + 1;
+            break;
+        }
+    }
+    if (np < 0) {
+        set_error("find_valid_octree_parents: coverage goal not reachable");
+        return false;
+    }
+    out->parents.assign(order.begin(), order.begin() + np);
+    out->rules.assign(tl, GroupRule{-1, 0, 0, 0, 0xFFFFFFFFu, 0u});
+    out->kept.assign(np, 0);
+    out->off.assign(np, 0.0);
+    out->search.clear();
+
+    std::vector<int> tail_fill(np), dangling(np, -1);
+    std::vector<char> is_parent(tl, 0);
+    for (int k = 0; k < np; k++) {
+        const int p = out->parents[k];
+        is_parent[p] = 1;
+        const long q = hist[p];
+        tail_fill[k] = q == 0 ? 0 : (int)((q - 1) % L) + 1;
+        out->rules[p].slot = k;
+        out->kept[k] = q;
+        out->off[k] = 180 - gc.h[p];
+    }
+    std::vector<double> dist(np);
+    for (int i = 0; i < tl; i++) {
+        if (hist[i] == 0 || is_parent[i]) continue;
+        double best = (double)tl * tl;                    // :368
+        int nmin = 0;
+        for (int k = 0; k < np; k++) {
+            const double d = node_distance(g, gc, i, out->parents[k]);
+            if (d < best) {
+                best = d;
+                nmin = 1;
+            } else if (d == best) {
+                nmin++;
+            }
+            dist[k] = d;
+        }
+        int k = 0;
+        while (dist[k] != best) k++;                      // first nearest, valid_parents order
+        const long n = hist[i];
+        GroupRule& r = out->rules[i];
+        r.slot = k;
+        if (dangling[k] >= 0) {                           // any event on k drops its dangling node
+            out->rules[dangling[k]].dangle = 0;
+            out->kept[k] -= 1;
+            dangling[k] = -1;
+        }
+        if (nmin > 1) {
+            const long room = L - tail_fill[k];
+            const long keep = n < room ? n : room;
+            tail_fill[k] += (int)keep;
+            out->kept[k] += keep;
+            if (keep < n) {
+                r.partial = 1;
+                r.keep = (int)keep;
+                r.cutoff = 0;                             // set on device when keep > 0
+                r.dangle = 1;
+                dangling[k] = i;
+                out->kept[k] += 1;
+            }
+        } else {
+            out->kept[k] += n;
+            tail_fill[k] = (int)((n - 1) % L) + 1;
+        }
+    }
+    for (int i = 0; i < tl; i++) {
+        const GroupRule& r = out->rules[i];
+        if (r.partial && (r.keep > 0 || r.dangle)) out->search.push_back(i);
+    }
+    return true;
+}
+
+}  // namespace phd

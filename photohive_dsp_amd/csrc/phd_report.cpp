@@ -1,0 +1,654 @@
+// phd_report.cpp -- the report pipeline and the exported C-ABI.
+//
+// Stage order of get_full_report_data (src/interface.c:20-94), per batch of
+// same-size device images on one stream:
+//
+//   K1  hsv/stats/histogram           every image        (palette.hip)
+//   D2H group histograms + moments    -> host decisions  (phd_palette.cpp)
+//   K4  FFT rows, K5 FFT columns      every image        (fft.hip)   || host decides
+//   H2D keep rules;  Kcut; K3 sums    every image        (palette.hip)
+//   sharpness (crops only)                                (sharpness.hip)
+//   D2H bins / max / palette sums -> host finalisation (G_s, averages, vectors)
+//
+// The FFT of an image depends only on K1's channel sums (for the DC bias), so
+// the host's palette decisions overlap the GPU's FFT work.
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <unistd.h>
+
+#include "phd_host.h"
+
+namespace phd {
+
+namespace {
+
+constexpr size_t kAlign = 256;
+size_t al(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+struct Layout {
+    // per-image records
+    size_t a_sums, a_hist, a_spart, a_bytes;                 // read back after K1 (zeroed)
+    size_t c_bins, c_fmax, c_pal, c_sharp, c_bytes;         // read back at the end (zeroed)
+    size_t b_rules, b_search, b_off, b_bytes;               // uploaded before K3
+    size_t chunk_bytes;                                      // device only
+    size_t dev_total, pin_total;
+    size_t A(int i) const { return (size_t)i * a_bytes; }
+    size_t C(int n, int i) const { return (size_t)n * a_bytes + (size_t)i * c_bytes; }
+    size_t B(int n, int i) const { return (size_t)n * (a_bytes + c_bytes) + (size_t)i * b_bytes; }
+    size_t H(int n, int i) const { return (size_t)n * (a_bytes + c_bytes + b_bytes) + (size_t)i * chunk_bytes; }
+};
+
+Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops) {
+    Layout L{};
+    L.a_sums = 0;
+    L.a_hist = al(6 * sizeof(unsigned long long));
+    L.a_spart = L.a_hist + al(sizeof(unsigned) * tl);
+    L.a_bytes = L.a_spart + al(sizeof(double) * nchunks);
+    L.c_bins = 0;
+    L.c_fmax = al(sizeof(double) * nbins);
+    L.c_pal = L.c_fmax + al(sizeof(unsigned long long));
+    L.c_sharp = L.c_pal + al(sizeof(double) * 4 * tl);
+    L.c_bytes = L.c_sharp + al(sizeof(double) * 2 * (ncrops > 0 ? ncrops : 1));
+    L.b_rules = 0;
+    L.b_search = al(sizeof(GroupRule) * tl);
+    L.b_off = L.b_search + al(sizeof(int) * tl);
+    L.b_bytes = L.b_off + al(sizeof(double) * tl);
+    L.chunk_bytes = al(sizeof(unsigned short) * (size_t)nchunks * tl);
+    L.dev_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes + L.chunk_bytes);
+    L.pin_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes);
+    return L;
+}
+
+bool check_crops(const Crop_Boundaries* cb, int height, int width) {
+    if (!cb) return true;
+    if (cb->N < 0 || (cb->N > 0 && (!cb->top || !cb->bottom || !cb->left || !cb->right))) {
+        set_error("Crop_Boundaries has NULL arrays");
+        return false;
+    }
+    for (int k = 0; k < cb->N; k++) {
+        const int t = cb->top[k], b = cb->bottom[k], l = cb->left[k], r = cb->right[k];
+        // crop_pgm's bounds test (src/image_processing.c:215-218); an empty or
+        // inverted box makes the reference divide by zero / misallocate.
+        if (r > width || l > width || b > height || t > height || l < 0 || r < 0 || t < 0 || b < 0 ||
+            r <= l || b <= t) {
+            set_error("crop boundaries outside of image boundaries (crop " + std::to_string(k) + ")");
+            return false;
+        }
+    }
+    return true;
+}
+
+// pre_compute_error_checks (src/utilities.c:64-87) on the dimensions.
+bool precheck(int height, int width) {
+    if (height < 350 || width < 350) {
+        set_error("Image height and width must be greater than 350. Height: " + std::to_string(height) +
+                  "\tWidth" + std::to_string(width));
+        return false;
+    }
+    if ((long long)height * width > 120000000LL) {
+        set_error("Image must have less than 120000000 pixels.");
+        return false;
+    }
+    const float ar = (float)height / (float)width;
+    if (ar < 1.0 / 5.0 || ar > 5.0 / 1.0) {
+        set_error("Invalid aspect ratio: " + std::to_string(ar));
+        return false;
+    }
+    return true;
+}
+
+long hsv_count(int height, int width, int ds) {
+    const int hh = ds > 1 ? height / ds : height, ww = ds > 1 ? width / ds : width;
+    return (long)(short)hh * (short)ww;
+}
+
+float ms_between(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return -1.f;
+    return ms;
+}
+
+Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const PaletteDecision& dec,
+                           const double* pal, long n_hsv, const BlurTable& tbl, const double* bin_sums,
+                           double fmax, const phd_config& cfg, const Crop_Boundaries* crops,
+                           const double* sharp_sums, std::string* why) {
+    const int np = (int)dec.parents.size();
+    // calculate_avg_hsv (src/color_quantization.c:510-576)
+    Color_Palette* cp = (Color_Palette*)malloc(sizeof(Color_Palette));
+    cp->N = np;
+    cp->averages = (Pixel_HSV*)malloc(sizeof(Pixel_HSV) * (np > 0 ? np : 1));
+    cp->percentages = (double*)malloc(sizeof(double) * (np > 0 ? np : 1));
+    const double inv_n = 1.0 / (int)n_hsv;
+    for (int k = 0; k < np; k++) {
+        const double cnt = pal[4 * k + 3];
+        if (cnt != (double)dec.kept[k]) {
+            *why = "palette self-check failed: device kept " + std::to_string((long long)cnt) +
+                   " pixels for slot " + std::to_string(k) + ", host rules predict " +
+                   std::to_string(dec.kept[k]);
+            free(cp->averages);
+            free(cp->percentages);
+            free(cp);
+            return nullptr;
+        }
+        const int tot = (int)dec.kept[k];
+        const double inv = 1.0 / (double)tot;
+        double h = pal[4 * k + 0] * inv;
+        h -= dec.off[k];
+        if (h < 0) h += 360;
+        else if (h > 360) h -= 360;
+        cp->averages[k].parent_id = dec.parents[k];   // uninitialised in the reference
+        cp->averages[k].h = h;
+        cp->averages[k].s = pal[4 * k + 1] * inv;
+        cp->averages[k].v = pal[4 * k + 2] * inv;
+        cp->percentages[k] = (double)tot * inv_n;
+    }
+    // pgm_normalize_fft's G_s (src/fft_processing.c:192) applied to the binned
+    // sums of log(p); calculate_blur_profile's averaging (src/blur_profile.c:106-116)
+    const int na = cfg.angle_partitions, nr = cfg.radius_partitions;
+    Blur_Profile* bp = (Blur_Profile*)malloc(sizeof(Blur_Profile));
+    bp->num_angle_bins = na;
+    bp->num_radius_bins = nr;
+    bp->angle_bin_size = tbl.angle_bin_size;
+    bp->radius_bin_size = tbl.radius_bin_size;
+    bp->bins = (Bin**)malloc(sizeof(Bin*) * na);
+    const double gs = 1 / (2 * std::log(std::sqrt(fmax) + 1));
+    std::vector<double> flat((size_t)na * nr);
+    for (int a = 0; a < na; a++) {
+        bp->bins[a] = (Bin*)calloc(nr, sizeof(Bin));
+        for (int r = 0; r < nr; r++) {
+            const size_t b = (size_t)a * nr + r;
+            const double q = (double)tbl.counts[b];
+            const double sum = bin_sums[b] == 0.0 ? 0.0 : bin_sums[b] * gs;
+            bp->bins[a][r] = q != 0 ? sum / q : 0;
+            flat[b] = bp->bins[a][r];
+        }
+    }
+    Blur_Vector_Group* bv = (Blur_Vector_Group*)calloc(1, sizeof(Blur_Vector_Group));
+    bv->len_vectors = 10;
+    bv->blur_vectors = (Blur_Vector*)calloc(10, sizeof(Blur_Vector));
+    vectorize_blur(flat.data(), na, nr, cfg.fft_streak_thresh, cfg.magnitude_thresh,
+                   cfg.blur_cutoff_ratio_denom, bv->blur_vectors);
+    Sharpnesses* sh = nullptr;
+    if (crops) {   // get_variance_sharpness (src/filtering.c:151-183)
+        sh = (Sharpnesses*)malloc(sizeof(Sharpnesses));
+        sh->N = crops->N;
+        sh->sharpness = (Pixel*)calloc(crops->N > 0 ? crops->N : 1, sizeof(Pixel));
+        for (int k = 0; k < crops->N; k++) {
+            const double cn = (double)((long)(crops->right[k] - crops->left[k]) *
+                                       (crops->bottom[k] - crops->top[k]));
+            const double avg = sharp_sums[2 * k] / cn;
+            const double var = sharp_sums[2 * k + 1] / cn;
+            sh->sharpness[k] = var / avg;
+        }
+    }
+    RGB_Statistics* rs = (RGB_Statistics*)calloc(1, sizeof(RGB_Statistics));
+    *rs = st;
+    Full_Report_Data* r = (Full_Report_Data*)malloc(sizeof(Full_Report_Data));
+    r->rgb_stats = rs;
+    r->color_palette = cp;
+    r->blur_profile = bp;
+    r->blur_vectors = bv;
+    r->average_saturation = s_bar;
+    r->sharpness = sh;
+    return r;
+}
+
+RGB_Statistics stats_from_sums(const unsigned long long* m, long n) {
+    // mean = sum(k)/255/N; population variance from exact integer moments:
+    // var = (N*sum(k^2) - sum(k)^2) / (255^2 N^2)   (filtering.c:125-148 in exact arithmetic)
+    RGB_Statistics s;
+    double* out = &s.Br;
+    for (int c = 0; c < 3; c++) {
+        out[c] = (double)m[c] / 255.0 / (double)n;
+        const unsigned __int128 num = (unsigned __int128)n * m[3 + c] - (unsigned __int128)m[c] * m[c];
+        const double var = (double)num / 65025.0 / ((double)n * (double)n);
+        out[3 + c] = std::sqrt(var);
+    }
+    return s;
+}
+
+}  // namespace
+
+bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, int width,
+                 const phd_config& cfg, const Crop_Boundaries* crops, Full_Report_Data** out, int* status,
+                 hipStream_t stream) {
+    const auto t_host0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n; i++) {
+        out[i] = nullptr;
+        status[i] = -1;
+    }
+    std::string why;
+    if (!validate_config(cfg, &why)) {
+        set_error(why);
+        return false;
+    }
+    if (!precheck(height, width) || !check_crops(crops, height, width)) return false;
+    if (width > kFftMaxLds || height > kFftMaxLds) {
+        set_error("image side above " + std::to_string(kFftMaxLds) +
+                  " px is not supported by this build's LDS-resident FFT");
+        return false;
+    }
+    const hipStream_t st = stream ? stream : c->stream;
+    const GridParams gp = make_grid(cfg);
+    const GroupCenters gc = make_centers(gp);
+    const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
+    const long n_hsv = hsv_count(height, width, ds);
+    const int nchunks = (int)((n_hsv + kChunk - 1) / kChunk);
+    const int nbins = cfg.radius_partitions * cfg.angle_partitions;
+    const int ncrops = crops ? crops->N : 0;
+    const int wf = width / 2 + 1;
+    const FftPlanHost* prow = get_plan(c, width);
+    const FftPlanHost* pcol = get_plan(c, height);
+    const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
+    if (!prow || !pcol || !tbl) return false;
+
+    const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops);
+    if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
+        !ensure_device((void**)&c->d_inter, &c->inter_bytes, sizeof(double2) * (size_t)height * wf))
+        return false;
+    uint8_t* dw = (uint8_t*)c->d_ws;
+    uint8_t* hp = (uint8_t*)c->h_pin;
+    std::vector<int> crop_arr;
+    if (ncrops) {
+        crop_arr.resize(4 * ncrops);
+        for (int k = 0; k < ncrops; k++) {
+            crop_arr[k] = crops->top[k];
+            crop_arr[ncrops + k] = crops->bottom[k];
+            crop_arr[2 * ncrops + k] = crops->left[k];
+            crop_arr[3 * ncrops + k] = crops->right[k];
+        }
+    }
+
+    PHD_HIP(hipMemsetAsync(dw, 0, (size_t)n * (L.a_bytes + L.c_bytes), st));
+    PHD_HIP(hipEventRecord(c->ev[0], st));
+    for (int i = 0; i < n; i++) {
+        PaletteDev pd;
+        pd.sums = (unsigned long long*)(dw + L.A(i) + L.a_sums);
+        pd.hist = (unsigned*)(dw + L.A(i) + L.a_hist);
+        pd.s_part = (double*)(dw + L.A(i) + L.a_spart);
+        pd.chunk_hist = (unsigned short*)(dw + L.H(n, i));
+        PHD_HIP(launch_hsv_stats(d_imgs[i], height, width, ds, gp, pd, nchunks, c->d_k255, st));
+    }
+    PHD_HIP(hipEventRecord(c->ev[1], st));
+    PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, st));
+    PHD_HIP(hipEventRecord(c->ev[5], st));
+    for (int i = 0; i < n; i++) {
+        const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+        double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
+        unsigned long long* fmx = (unsigned long long*)(dw + L.C(n, i) + L.c_fmax);
+        PHD_HIP(launch_fft_rows(d_imgs[i], height, width, prow->plan, sums, c->d_k255, c->d_inter, st));
+        PHD_HIP(launch_fft_cols(c->d_inter, height, wf, pcol->plan, tbl->d_map, nbins, bins, fmx, st));
+        if (ncrops) {
+            // crop boxes: sharpness on the full-resolution luma before DC removal
+            PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
+                                     crop_arr.data() + ncrops, crop_arr.data() + 2 * ncrops,
+                                     crop_arr.data() + 3 * ncrops, c->d_k255,
+                                     (double*)(dw + L.C(n, i) + L.c_sharp), st));
+        }
+    }
+    PHD_HIP(hipEventRecord(c->ev[2], st));
+
+    // host decisions while the FFTs run
+    PHD_HIP(hipEventSynchronize(c->ev[5]));
+    std::vector<PaletteDecision> dec(n);
+    std::vector<int> ok(n, 1);
+    for (int i = 0; i < n; i++) {
+        const unsigned* hist = (const unsigned*)(hp + L.A(i) + L.a_hist);
+        if (!decide_palette(gp, gc, hist, n_hsv, cfg, &dec[i])) {
+            ok[i] = 0;
+            continue;
+        }
+        uint8_t* b = hp + L.pin_total - (size_t)n * L.b_bytes + (size_t)i * L.b_bytes;
+        memcpy(b + L.b_rules, dec[i].rules.data(), sizeof(GroupRule) * gp.tl);
+        memcpy(b + L.b_search, dec[i].search.data(), sizeof(int) * dec[i].search.size());
+        memcpy(b + L.b_off, dec[i].off.data(), sizeof(double) * dec[i].off.size());
+    }
+    uint8_t* hb = hp + L.pin_total - (size_t)n * L.b_bytes;
+    PHD_HIP(hipMemcpyAsync(dw + L.B(n, 0), hb, (size_t)n * L.b_bytes, hipMemcpyHostToDevice, st));
+    for (int i = 0; i < n; i++) {
+        if (!ok[i]) continue;
+        GroupRule* rules = (GroupRule*)(dw + L.B(n, i) + L.b_rules);
+        const int* search = (const int*)(dw + L.B(n, i) + L.b_search);
+        const double* off = (const double*)(dw + L.B(n, i) + L.b_off);
+        PHD_HIP(launch_palette_cutoffs(d_imgs[i], height, width, ds, gp,
+                                       (const unsigned short*)(dw + L.H(n, i)), nchunks, rules, search,
+                                       (int)dec[i].search.size(), c->d_k255, st));
+        PHD_HIP(launch_palette_sums(d_imgs[i], height, width, ds, gp, rules, off,
+                                    (int)dec[i].parents.size(), (double*)(dw + L.C(n, i) + L.c_pal),
+                                    c->d_k255, st));
+    }
+    PHD_HIP(hipEventRecord(c->ev[3], st));
+    uint8_t* hc = hp + (size_t)n * L.a_bytes;
+    PHD_HIP(hipMemcpyAsync(hc, dw + L.C(n, 0), (size_t)n * L.c_bytes, hipMemcpyDeviceToHost, st));
+    PHD_HIP(hipEventRecord(c->ev[4], st));
+    PHD_HIP(hipEventSynchronize(c->ev[4]));
+
+    int failures = 0;
+    for (int i = 0; i < n; i++) {
+        if (!ok[i]) {
+            failures++;
+            continue;
+        }
+        const uint8_t* a = hp + L.A(i);
+        const uint8_t* cc = hc + (size_t)i * L.c_bytes;
+        const unsigned long long* sums = (const unsigned long long*)(a + L.a_sums);
+        const double* spart = (const double*)(a + L.a_spart);
+        double s_acc = 0.0;
+        for (int k = 0; k < nchunks; k++) s_acc += spart[k];
+        const RGB_Statistics st_i = stats_from_sums(sums, (long)height * width);
+        unsigned long long fbits;
+        memcpy(&fbits, cc + L.c_fmax, sizeof(fbits));
+        double fmax;
+        memcpy(&fmax, &fbits, sizeof(fmax));
+        std::string w;
+        out[i] = assemble(st_i, s_acc / (double)n_hsv, dec[i], (const double*)(cc + L.c_pal), n_hsv, *tbl,
+                          (const double*)(cc + L.c_bins), fmax, cfg, crops,
+                          (const double*)(cc + L.c_sharp), &w);
+        if (!out[i]) {
+            set_error(w);
+            failures++;
+        } else {
+            status[i] = 0;
+        }
+    }
+    const double host_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+    double tm[5] = {ms_between(c->ev[0], c->ev[1]), ms_between(c->ev[1], c->ev[2]),
+                    ms_between(c->ev[2], c->ev[3]), ms_between(c->ev[0], c->ev[4]), host_ms};
+    record_timings(tm, 5);
+    return failures == 0;
+}
+
+bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, const phd_config& cfg,
+                       std::vector<unsigned>* hist, PaletteDecision* dec, std::vector<double>* dcounts) {
+    std::string why;
+    if (!validate_config(cfg, &why)) {
+        set_error(why);
+        return false;
+    }
+    const hipStream_t st = c->stream;
+    const GridParams gp = make_grid(cfg);
+    const GroupCenters gc = make_centers(gp);
+    const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
+    const long n_hsv = hsv_count(height, width, ds);
+    const int nchunks = (int)((n_hsv + kChunk - 1) / kChunk);
+    const Layout L = make_layout(1, gp.tl, nchunks, 1, 0);
+    if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total)) return false;
+    uint8_t* dw = (uint8_t*)c->d_ws;
+    uint8_t* hp = (uint8_t*)c->h_pin;
+    PHD_HIP(hipMemsetAsync(dw, 0, L.a_bytes + L.c_bytes, st));
+    PaletteDev pd;
+    pd.sums = (unsigned long long*)(dw + L.a_sums);
+    pd.hist = (unsigned*)(dw + L.a_hist);
+    pd.s_part = (double*)(dw + L.a_spart);
+    pd.chunk_hist = (unsigned short*)(dw + L.H(1, 0));
+    PHD_HIP(launch_hsv_stats(d_img, height, width, ds, gp, pd, nchunks, c->d_k255, st));
+    PHD_HIP(hipMemcpyAsync(hp, dw, L.a_bytes, hipMemcpyDeviceToHost, st));
+    PHD_HIP(hipStreamSynchronize(st));
+    hist->assign((const unsigned*)(hp + L.a_hist), (const unsigned*)(hp + L.a_hist) + gp.tl);
+    if (!decide_palette(gp, gc, hist->data(), n_hsv, cfg, dec)) return false;
+    uint8_t* b = hp + L.a_bytes + L.c_bytes;
+    memcpy(b + L.b_rules, dec->rules.data(), sizeof(GroupRule) * gp.tl);
+    memcpy(b + L.b_search, dec->search.data(), sizeof(int) * dec->search.size());
+    memcpy(b + L.b_off, dec->off.data(), sizeof(double) * dec->off.size());
+    PHD_HIP(hipMemcpyAsync(dw + L.B(1, 0), b, L.b_bytes, hipMemcpyHostToDevice, st));
+    GroupRule* rules = (GroupRule*)(dw + L.B(1, 0) + L.b_rules);
+    PHD_HIP(launch_palette_cutoffs(d_img, height, width, ds, gp, pd.chunk_hist, nchunks, rules,
+                                   (const int*)(dw + L.B(1, 0) + L.b_search), (int)dec->search.size(),
+                                   c->d_k255, st));
+    PHD_HIP(launch_palette_sums(d_img, height, width, ds, gp, rules, (const double*)(dw + L.B(1, 0) + L.b_off),
+                                (int)dec->parents.size(), (double*)(dw + L.C(1, 0) + L.c_pal), c->d_k255, st));
+    const int np = (int)dec->parents.size();
+    std::vector<double> pal(4 * np);
+    PHD_HIP(hipMemcpyAsync(pal.data(), dw + L.C(1, 0) + L.c_pal, sizeof(double) * 4 * np,
+                           hipMemcpyDeviceToHost, st));
+    PHD_HIP(hipStreamSynchronize(st));
+    dcounts->resize(np);
+    for (int k = 0; k < np; k++) (*dcounts)[k] = pal[4 * k + 3];
+    return true;
+}
+
+}  // namespace phd
+
+// ============================================================================
+// exported C-ABI
+// ============================================================================
+using namespace phd;
+
+extern "C" void phd_config_default(phd_config* c) {
+    // get_report defaults, /root/reference/core.py:442-448
+    c->h_partitions = 18;
+    c->s_partitions = 2;
+    c->v_partitions = 3;
+    c->black_thresh = 0.1;
+    c->gray_thresh = 0.1;
+    c->coverage_thresh = 0.95;
+    c->linked_list_size = 1000;
+    c->downsample_rate = 1;
+    c->radius_partitions = 40;
+    c->angle_partitions = 72;
+    c->quantity_weight = 0.1f;
+    c->saturation_value_weight = 0.9f;
+    c->fft_streak_thresh = 1.20;
+    c->magnitude_thresh = 0.3;
+    c->blur_cutoff_ratio_denom = 2;
+}
+
+static Full_Report_Data* report_from_host(const uint8_t* rgb, int height, int width, size_t row_stride,
+                                          const phd_config* cfg, const Crop_Boundaries* crops) {
+    clear_error();
+    if (!rgb || !cfg) {
+        set_error("Error: Image pointer is NULL.");
+        return nullptr;
+    }
+    if (!precheck(height, width)) return nullptr;
+    Context* c = get_context();
+    if (!c) return nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    const size_t row = 3 * (size_t)width;
+    const size_t bytes = row * height;
+    if (!ensure_device((void**)&c->d_stage, &c->stage_bytes, bytes)) return nullptr;
+    hipError_t e;
+    if (row_stride == 0 || row_stride == row)
+        e = hipMemcpyAsync(c->d_stage, rgb, bytes, hipMemcpyHostToDevice, c->stream);
+    else
+        e = hipMemcpy2DAsync(c->d_stage, row, rgb, row_stride, row, height, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+        set_error(std::string("upload failed: ") + hipGetErrorString(e));
+        return nullptr;
+    }
+    const uint8_t* imgs[1] = {c->d_stage};
+    Full_Report_Data* out = nullptr;
+    int status = -1;
+    run_reports(c, imgs, 1, height, width, *cfg, crops, &out, &status, nullptr);
+    // the caller's buffer may be freed on return: drain the upload on every path
+    (void)hipStreamSynchronize(c->stream);
+    return out;
+}
+
+extern "C" Full_Report_Data* phd_report_u8(const uint8_t* rgb, int height, int width, size_t row_stride,
+                                           const phd_config* cfg, const Crop_Boundaries* crops) {
+    return report_from_host(rgb, height, width, row_stride, cfg, crops);
+}
+
+extern "C" Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundaries* crops, int h_partitions,
+                                                  int s_partitions, int v_partitions, double black_thresh,
+                                                  double gray_thresh, double coverage_thresh,
+                                                  int linked_list_size, int downsample_rate,
+                                                  int radius_partitions, int angle_partitions,
+                                                  float quantity_weight, float saturation_value_weight,
+                                                  double fft_streak_thresh, double magnitude_thresh,
+                                                  int blur_cutoff_ratio_denom) {
+    clear_error();
+    // pre_compute_error_checks (src/utilities.c:64-87), same order and messages
+    if (!image) {
+        set_error("Error: Image pointer is NULL.");
+        return nullptr;
+    }
+    if (!precheck(image->height, image->width)) return nullptr;
+    if (!image->r || !image->g || !image->b) {
+        set_error("Error: At least one color channel was a NULL pointer.");
+        return nullptr;
+    }
+    phd_config cfg{h_partitions, s_partitions, v_partitions, black_thresh, gray_thresh, coverage_thresh,
+                   linked_list_size, downsample_rate, radius_partitions, angle_partitions,
+                   quantity_weight, saturation_value_weight, fft_streak_thresh, magnitude_thresh,
+                   blur_cutoff_ratio_denom};
+    if (getenv("PHD_VERBOSE"))   // interface.c:34-35 prints this unconditionally
+        printf("\n There are %d cores available to the C program.\n\n", (int)sysconf(_SC_NPROCESSORS_ONLN));
+    // planar doubles (utils.py:30-46 produces k/255.0) -> interleaved RGB8
+    const size_t n = (size_t)image->height * image->width;
+    std::vector<uint8_t> rgb(3 * n);
+    const Pixel* ch[3] = {image->r, image->g, image->b};
+    for (int c = 0; c < 3; c++)
+        for (size_t i = 0; i < n; i++) {
+            const double x = ch[c][i];
+            const long k = std::lround(x * 255.0);
+            if (k < 0 || k > 255 || (double)k / 255.0 != x) {
+                set_error("get_full_report_data: channel values must be k/255.0 for integer k in [0,255] "
+                          "(8-bit images); arbitrary doubles are not supported by the MI355X path");
+                return nullptr;
+            }
+            rgb[3 * i + c] = (uint8_t)k;
+        }
+    return report_from_host(rgb.data(), image->height, image->width, 0, &cfg, crops);
+}
+
+extern "C" void free_full_report(Full_Report_Data** report) {
+    // src/interface.c:97-111
+    if (!report || !*report) return;
+    Full_Report_Data* r = *report;
+    if (r->color_palette) {
+        free(r->color_palette->averages);
+        free(r->color_palette->percentages);
+        free(r->color_palette);
+    }
+    if (r->blur_profile) {
+        for (int a = 0; a < r->blur_profile->num_angle_bins; a++) free(r->blur_profile->bins[a]);
+        free(r->blur_profile->bins);
+        free(r->blur_profile);
+    }
+    if (r->blur_vectors) {
+        free(r->blur_vectors->blur_vectors);
+        free(r->blur_vectors);
+    }
+    if (r->sharpness) {
+        free(r->sharpness->sharpness);
+        free(r->sharpness);
+    }
+    free(r->rgb_stats);
+    free(r);
+    *report = nullptr;
+}
+
+extern "C" int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
+                                       size_t image_stride, const phd_config* cfg, Full_Report_Data** out,
+                                       int* status, void* stream) {
+    clear_error();
+    if (!d_rgb || !cfg || !out || !status || n_images <= 0) {
+        set_error("phd_report_batch_device: bad arguments");
+        return -1;
+    }
+    Context* c = get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
+    std::vector<const uint8_t*> imgs(n_images);
+    for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
+    run_reports(c, imgs.data(), n_images, height, width, *cfg, nullptr, out, status, (hipStream_t)stream);
+    int fails = 0;
+    for (int i = 0; i < n_images; i++) fails += status[i] != 0;
+    return fails;
+}
+
+extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
+                                   int n_images, const phd_config* cfg, Full_Report_Data** out, int* status) {
+    clear_error();
+    if (!images || !heights || !widths || !cfg || !out || !status || n_images <= 0) {
+        set_error("phd_report_batch_u8: bad arguments");
+        return -1;
+    }
+    int fails = 0;
+    for (int i = 0; i < n_images; i++) {
+        out[i] = report_from_host(images[i], heights[i], widths[i], 0, cfg, nullptr);
+        status[i] = out[i] ? 0 : -1;
+        fails += !out[i];
+    }
+    return fails;
+}
+
+extern "C" int phd_palette_trace_device(const uint8_t* d_rgb, int height, int width, const phd_config* cfg,
+                                        int* hist, int* parents, int* kept, int* n_parents) {
+    clear_error();
+    Context* c = get_context();
+    if (!c || !cfg) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    std::vector<unsigned> h;
+    PaletteDecision dec;
+    std::vector<double> dcount;
+    if (!run_palette_trace(c, d_rgb, height, width, *cfg, &h, &dec, &dcount)) return -1;
+    const int np = (int)dec.parents.size();
+    for (size_t g = 0; g < h.size(); g++) hist[g] = (int)h[g];
+    for (int k = 0; k < np; k++) {
+        parents[k] = dec.parents[k];
+        kept[k] = (int)dcount[k];     // what the device actually summed
+    }
+    *n_parents = np;
+    for (int k = 0; k < np; k++)
+        if (dcount[k] != (double)dec.kept[k]) {
+            set_error("device kept count differs from the host keep rules");
+            return -2;
+        }
+    return (int)h.size();
+}
+
+extern "C" int phd_blur_counts(int height, int width, int radius_partitions, int angle_partitions,
+                               long long* counts) {
+    clear_error();
+    Context* c = get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    const BlurTable* tb = get_table(c, height, width, radius_partitions, angle_partitions);
+    if (!tb) return -1;
+    memcpy(counts, tb->counts.data(), sizeof(long long) * tb->counts.size());
+    return 0;
+}
+
+extern "C" int phd_fill_uniform_device(uint8_t* d_dst, size_t n, uint64_t seed, void* stream) {
+    clear_error();
+    Context* c = get_context();
+    if (!c) return -1;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (launch_fill_uniform(d_dst, n, seed, st) != hipSuccess) {
+        set_error("fill kernel launch failed");
+        return -1;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        set_error("fill kernel failed");
+        return -1;
+    }
+    return 0;
+}
+
+extern "C" int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, const phd_config* cfg, int* d_gid,
+                                           double* d_hsv) {
+    clear_error();
+    Context* c = get_context();
+    if (!c || !cfg) return -1;
+    std::string why;
+    if (!validate_config(*cfg, &why)) {
+        set_error(why);
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    const GridParams gp = make_grid(*cfg);
+    if (launch_debug_hsv(d_rgb, n_pixels, gp, c->d_k255, d_gid, d_hsv, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        set_error("debug hsv kernel failed");
+        return -1;
+    }
+    return 0;
+}

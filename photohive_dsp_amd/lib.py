@@ -1,0 +1,79 @@
+"""Loads PhotoHive_DSP_lib/libreport_data.so (the MI355X build) -- same path
+and argtypes as /root/reference/lib.py:20-37, plus the new entry points."""
+import ctypes
+import os
+
+from .structures import (Blur_Profile, Crop_Boundaries, Full_Report_Data, Image_PGM, Image_RGB,
+                         PhdConfig)
+
+def _preload_torch_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64.so
+    (SONAME libamdhip64.so.7) and its libraries NEED the unversioned name; if
+    this library were loaded first it would bind /opt/rocm's copy and torch
+    would then load a second runtime.  Loading torch's file first (without
+    importing torch) makes both resolve to the same runtime."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    cand = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(cand):
+        ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+
+
+_preload_torch_hip_runtime()
+directory = os.path.dirname(os.path.abspath(__file__))
+lib_path = os.path.join(directory, "PhotoHive_DSP_lib/libreport_data.so")
+if not os.path.exists(lib_path):
+    raise ImportError(f"{lib_path} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "or `make -C photohive_dsp_amd/csrc` (there is no CPU fallback)")
+lib = ctypes.CDLL(lib_path)
+
+P = ctypes.POINTER
+lib.get_full_report_data.restype = P(Full_Report_Data)
+lib.get_full_report_data.argtypes = [
+    P(Image_RGB), P(Crop_Boundaries),
+    ctypes.c_int, ctypes.c_int, ctypes.c_int,
+    ctypes.c_double, ctypes.c_double,
+    ctypes.c_double, ctypes.c_int,
+    ctypes.c_int, ctypes.c_int, ctypes.c_int,
+    ctypes.c_float, ctypes.c_float,
+    ctypes.c_double, ctypes.c_double, ctypes.c_int,
+]
+lib.get_blur_profile_visual.restype = P(Image_PGM)
+lib.get_blur_profile_visual.argtypes = [P(Blur_Profile), ctypes.c_int, ctypes.c_int]
+
+# new entry points (include/photohive_dsp.h)
+lib.phd_config_default.argtypes = [P(PhdConfig)]
+lib.phd_report_u8.restype = P(Full_Report_Data)
+lib.phd_report_u8.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, P(PhdConfig),
+                              P(Crop_Boundaries)]
+lib.phd_report_batch_device.restype = ctypes.c_int
+lib.phd_report_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_size_t, P(PhdConfig), P(P(Full_Report_Data)),
+                                        P(ctypes.c_int), ctypes.c_void_p]
+lib.phd_report_batch_u8.restype = ctypes.c_int
+lib.phd_report_batch_u8.argtypes = [P(ctypes.c_void_p), P(ctypes.c_int), P(ctypes.c_int), ctypes.c_int,
+                                    P(PhdConfig), P(P(Full_Report_Data)), P(ctypes.c_int)]
+lib.phd_palette_trace_device.restype = ctypes.c_int
+lib.phd_palette_trace_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(PhdConfig),
+                                         P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int)]
+lib.phd_blur_counts.restype = ctypes.c_int
+lib.phd_blur_counts.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(ctypes.c_longlong)]
+lib.phd_fill_uniform_device.restype = ctypes.c_int
+lib.phd_fill_uniform_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]
+lib.phd_debug_hsv_groups_device.restype = ctypes.c_int
+lib.phd_debug_hsv_groups_device.argtypes = [ctypes.c_void_p, ctypes.c_long, P(PhdConfig), ctypes.c_void_p,
+                                            ctypes.c_void_p]
+lib.free_full_report.restype = None
+lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
+lib.phd_free_pgm.argtypes = [P(Image_PGM)]
+lib.phd_last_error.restype = ctypes.c_char_p
+lib.phd_device_info.restype = ctypes.c_int
+lib.phd_device_info.argtypes = [ctypes.c_char_p, ctypes.c_int]
+lib.phd_last_timings.restype = ctypes.c_int
+lib.phd_last_timings.argtypes = [P(ctypes.c_double), ctypes.c_int]
+
+
+def last_error() -> str:
+    return (lib.phd_last_error() or b"").decode()

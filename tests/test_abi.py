@@ -1,0 +1,85 @@
+"""C-ABI surface (CPU): the library loads and exports every symbol
+include/photohive_dsp.h declares; struct layouts match the reference's
+ctypes binding; no GPU => loud failure, never a silent CPU fallback."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "photohive_dsp.h")
+SO = os.path.join(ROOT, "photohive_dsp_amd", "PhotoHive_DSP_lib", "libreport_data.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\((?=[^;{]*\)\s*;)", src)
+    keywords = {"if", "for", "while", "return", "sizeof"}
+    return sorted({n for n in names if n not in keywords})
+
+
+def test_header_declares_reference_entry_points():
+    fns = declared_functions()
+    for f in ("get_full_report_data", "free_full_report", "get_blur_profile_visual"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(SO), "run __graft_entry__.build() first"
+    lib = ctypes.CDLL(SO)
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+
+
+def test_struct_layouts_match_reference_binding():
+    from photohive_dsp_amd import structures as S
+    # x86-64 sizes of the reference structs (src/*.h)
+    assert ctypes.sizeof(S.Pixel_HSV) == 32
+    assert ctypes.sizeof(S.Image_RGB) == 32
+    assert ctypes.sizeof(S.Image_PGM) == 16
+    assert ctypes.sizeof(S.RGB_Statistics) == 48
+    assert ctypes.sizeof(S.Crop_Boundaries) == 40
+    assert ctypes.sizeof(S.Color_Palette) == 24
+    assert ctypes.sizeof(S.Blur_Profile) == 24
+    assert ctypes.sizeof(S.Blur_Vector) == 8
+    assert ctypes.sizeof(S.Blur_Vector_Group) == 16
+    assert ctypes.sizeof(S.Sharpnesses) == 16
+    assert ctypes.sizeof(S.Full_Report_Data) == 48
+    assert S.Full_Report_Data.average_saturation.offset == 32
+
+
+def test_config_defaults_match_get_report():
+    from photohive_dsp_amd.lib import lib
+    from photohive_dsp_amd.structures import PhdConfig
+    from photohive_dsp_amd.core import make_config
+    c = PhdConfig()
+    lib.phd_config_default(ctypes.byref(c))
+    d = make_config()
+    for f, _ in PhdConfig._fields_:
+        assert getattr(c, f) == getattr(d, f), f
+
+
+def test_no_silent_cpu_fallback():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import photohive_dsp_amd as phd
+    from photohive_dsp_amd.lib import last_error
+    from photohive_dsp_amd import synth
+    with pytest.raises(ValueError):
+        phd.get_report(synth.uniform(400, 400, 1))
+    assert "no HIP device" in last_error()
+
+
+def test_reference_rejections_are_null_before_touching_gpu():
+    """pre_compute_error_checks (src/utilities.c:64-87) paths return NULL."""
+    import numpy as np
+    import photohive_dsp_amd as phd
+    from photohive_dsp_amd.lib import last_error
+    for h, w in [(349, 350), (350, 349), (2001, 400), (400, 2001)]:
+        with pytest.raises(ValueError):
+            phd.get_report(np.zeros((h, w, 3), np.uint8))
+        assert "350" in last_error() or "aspect" in last_error()

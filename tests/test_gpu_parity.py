@@ -1,0 +1,209 @@
+"""GPU parity: the HIP path through the C-ABI against the reference's golden
+vectors (tests/golden, produced by the reference's own C) and the CPU oracle.
+
+Bars (BASELINE.json north_star): histogram counts, palette group ids/order,
+kept-pixel counts, blur bin counts and percentages bit-exact; float fields
+within 1e-4 relative (observed ~1e-12: fp64 everywhere, only summation order
+and libm ulps differ).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests.conftest import golden_case, golden_image, golden_manifest
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_RTOL = 1e-4          # north_star tolerance for float fields
+TIGHT_RTOL = 1e-9          # what fp64 actually delivers; tracked, not the contract
+
+CASES = golden_manifest()["cases"]
+
+
+def _phd():
+    import photohive_dsp_amd as phd
+    from photohive_dsp_amd import lib as L
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return phd, L, torch
+
+
+def _crops(case):
+    from photohive_dsp_amd import set_bounding_boxes
+    return set_bounding_boxes(case["crops"]) if case["crops"] else None
+
+
+def _trace(img, **kw):
+    """palette intermediates (hist, parents, kept) of the device path."""
+    phd, L, torch = _phd()
+    from photohive_dsp_amd.core import make_config
+    cfg = make_config(**kw)
+    t = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+    tl = cfg.h_partitions * cfg.s_partitions * cfg.v_partitions + cfg.v_partitions + 1
+    hist = (ctypes.c_int * tl)()
+    parents = (ctypes.c_int * tl)()
+    kept = (ctypes.c_int * tl)()
+    npar = ctypes.c_int()
+    rc = L.lib.phd_palette_trace_device(t.data_ptr(), img.shape[0], img.shape[1], ctypes.byref(cfg),
+                                        hist, parents, kept, ctypes.byref(npar))
+    assert rc == tl, L.last_error()
+    n = npar.value
+    return np.array(hist[:]), np.array(parents[:n]), np.array(kept[:n])
+
+
+def assert_report_matches(rep, g, rtol=FLOAT_RTOL):
+    st = rep.rgb_stats
+    np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], g["stats"], rtol=rtol, atol=1e-15)
+    np.testing.assert_allclose(rep.average_saturation, float(g["average_saturation"]), rtol=rtol, atol=1e-15)
+    cp = rep.color_palette
+    # palette indices and order: bit-exact
+    np.testing.assert_array_equal(np.array(cp.group_ids), g["valid_parents"])
+    # percentages = kept/N: bit-exact
+    np.testing.assert_array_equal(np.array(cp.quantities), g["palette_pct"])
+    np.testing.assert_allclose(np.array(cp.hsv).reshape(-1, 3), g["palette_hsv"], rtol=rtol, atol=1e-12)
+    bins = np.array(rep.blur_profile.bins)
+    np.testing.assert_allclose(bins, g["bins"], rtol=rtol, atol=1e-12)
+    np.testing.assert_array_equal([v.angle for v in rep.blur_vectors], g["blur_angles"])
+    np.testing.assert_array_equal(np.array([v.magnitude for v in rep.blur_vectors], np.float32), g["blur_mags"])
+    assert rep.bp_ptr.angle_bin_size == int(g["angle_bin_size"])
+    assert rep.bp_ptr.radius_bin_size == int(g["radius_bin_size"])
+    if "sharpness" in g:
+        np.testing.assert_allclose(rep.sharpnesses, g["sharpness"], rtol=rtol)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_report_matches_reference_fixture(case):
+    phd, L, _ = _phd()
+    g = golden_case(case["name"])
+    img = golden_image(case)
+    rep = phd.get_report(img, salient_characters=_crops(case), **case["config"])
+    assert_report_matches(rep, g)
+    # and the tighter bar fp64 actually reaches (reported separately for the record)
+    st = rep.rgb_stats
+    np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], g["stats"], rtol=TIGHT_RTOL)
+    np.testing.assert_allclose(np.array(rep.blur_profile.bins), g["bins"], rtol=TIGHT_RTOL, atol=1e-14)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_palette_intermediates_bit_exact(case):
+    g = golden_case(case["name"])
+    img = golden_image(case)
+    hist, parents, kept = _trace(img, **case["config"])
+    np.testing.assert_array_equal(hist, g["hist"])
+    np.testing.assert_array_equal(parents, g["valid_parents"])
+    np.testing.assert_array_equal(kept, g["kept"])
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if not c["config"].get("downsample_rate")][:6],
+                         ids=lambda c: c["name"])
+def test_blur_counts_bit_exact(case):
+    phd, L, _ = _phd()
+    g = golden_case(case["name"])
+    na = case["config"].get("angle_partitions", 72)
+    nr = case["config"].get("radius_partitions", 40)
+    counts = (ctypes.c_longlong * (na * nr))()
+    assert L.lib.phd_blur_counts(case["height"], case["width"], nr, na, counts) == 0
+    np.testing.assert_array_equal(np.array(counts[:]).reshape(na, nr), g["bin_counts"])
+
+
+def test_legacy_planar_double_entry_point():
+    """get_full_report_data with the reference binding's planar doubles (utils.py:30-46)."""
+    phd, L, _ = _phd()
+    from photohive_dsp_amd.utils import pil_image_to_image_rgb
+    from PIL import Image
+    case = [c for c in CASES if c["name"] == "structured_384x512"][0]
+    g = golden_case(case["name"])
+    pil = Image.fromarray(golden_image(case))
+    im = pil_image_to_image_rgb(pil)
+    ptr = L.lib.get_full_report_data(ctypes.byref(im), None, 18, 2, 3, 0.1, 0.1, 0.95, 1000, 1, 40, 72,
+                                     0.1, 0.9, 1.20, 0.3, 2)
+    rep = phd.Report(ptr, case["height"], case["width"])
+    assert_report_matches(rep, g)
+
+
+def test_batch_device_matches_single_reports():
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    imgs = [synth.make(k, 480, 640, s) for k, s in [("uniform", 1), ("structured", 2), ("hblur", 3)]]
+    t = torch.from_numpy(np.stack(imgs)).cuda()
+    batch = phd.report_device(t)
+    for img, rb in zip(imgs, batch):
+        rs = phd.get_report(img)
+        assert rs.color_palette.group_ids == rb.color_palette.group_ids
+        assert rs.color_palette.quantities == rb.color_palette.quantities
+        np.testing.assert_allclose(np.array(rb.blur_profile.bins), np.array(rs.blur_profile.bins), rtol=1e-12,
+                                   atol=1e-14)
+
+
+def test_mixed_size_host_batch():
+    phd, L, _ = _phd()
+    from photohive_dsp_amd import synth
+    from oracle import oracle as orc
+    imgs = [synth.make("structured", h, w, s) for (h, w, s) in [(512, 512, 1), (480, 640, 2), (720, 1280, 3)]]
+    reps = phd.get_reports(imgs, h_partitions=36, s_partitions=4, v_partitions=5)
+    for img, r in zip(imgs, reps):
+        o = orc.report(img, h_partitions=36, s_partitions=4, v_partitions=5)
+        np.testing.assert_array_equal(np.array(r.color_palette.group_ids), o.valid_parents)
+        np.testing.assert_array_equal(np.array(r.color_palette.quantities), o.palette_pct)
+        np.testing.assert_allclose(np.array(r.blur_profile.bins), o.bins, rtol=FLOAT_RTOL, atol=1e-12)
+
+
+def test_rejections_return_null():
+    phd, L, _ = _phd()
+    for h, w in [(349, 350), (2001, 400), (400, 2001)]:
+        with pytest.raises(ValueError):
+            phd.get_report(np.zeros((h, w, 3), np.uint8))
+
+
+def test_device_synthetic_fill_matches_numpy():
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    n = 3 * 401 * 577
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    assert L.lib.phd_fill_uniform_device(t.data_ptr(), n, 7, None) == 0
+    np.testing.assert_array_equal(t.cpu().numpy(), synth.uniform(401, 577, 7).ravel())
+
+
+@pytest.mark.parametrize("kind,seed", [("uniform", 1), ("structured", 2), ("dominant", 3)])
+def test_full_size_4000x3000_against_oracle(kind, seed):
+    """BASELINE config 2 size: the whole report against the CPU oracle."""
+    phd, L, _ = _phd()
+    from photohive_dsp_amd import synth
+    from oracle import oracle as orc
+    img = synth.make(kind, 3000, 4000, seed)
+    rep = phd.get_report(img)
+    o = orc.report(img, fft_workers=8)
+    hist, parents, kept = _trace(img)
+    np.testing.assert_array_equal(hist, o.hist)
+    np.testing.assert_array_equal(parents, o.valid_parents)
+    np.testing.assert_array_equal(kept, o.kept)
+    g = dict(stats=o.stats, average_saturation=np.array(o.average_saturation), valid_parents=o.valid_parents,
+             palette_pct=o.palette_pct, palette_hsv=o.palette_hsv, bins=o.bins, blur_angles=o.blur_angles,
+             blur_mags=o.blur_mags, angle_bin_size=np.array(o.angle_bin_size),
+             radius_bin_size=np.array(o.radius_bin_size))
+    assert_report_matches(rep, g)
+
+
+@pytest.mark.parametrize("cfg", [{}, {"h_partitions": 36, "s_partitions": 4, "v_partitions": 5},
+                                 {"black_thresh": 0.25, "gray_thresh": 0.2, "h_partitions": 12}],
+                         ids=["default", "36_4_5", "thresholds"])
+def test_hsv_group_exhaustive_rgb_cube(cfg):
+    """Device rgb2hsv + arm_octree group id == the C oracle for all 2^24 RGB8 triples."""
+    phd, L, torch = _phd()
+    from oracle import oracle as orc
+    from photohive_dsp_amd.core import make_config
+    k = np.arange(1 << 24, dtype=np.uint32)
+    cube = np.stack([(k >> 16) & 255, (k >> 8) & 255, k & 255], axis=1).astype(np.uint8)
+    want, want_hsv = orc.group_ids(cube, with_hsv=True, **cfg)
+    d_rgb = torch.from_numpy(cube).cuda()
+    d_gid = torch.empty(1 << 24, dtype=torch.int32, device="cuda")
+    d_hsv = torch.empty((1 << 24, 3), dtype=torch.float64, device="cuda")
+    c = make_config(**cfg)
+    assert L.lib.phd_debug_hsv_groups_device(d_rgb.data_ptr(), 1 << 24, ctypes.byref(c), d_gid.data_ptr(),
+                                             d_hsv.data_ptr()) == 0
+    got_hsv = d_hsv.cpu().numpy()
+    bad = np.nonzero(np.any(got_hsv != want_hsv, axis=1))[0]
+    assert bad.size == 0, f"{bad.size} hsv mismatches, e.g. rgb={cube[bad[:5]].tolist()} " \
+                          f"gpu={got_hsv[bad[:3]].tolist()} cpu={want_hsv[bad[:3]].tolist()}"
+    np.testing.assert_array_equal(d_gid.cpu().numpy(), want)
