@@ -184,6 +184,14 @@ int phd_device_info(char* buf, int buflen);
  * [3] palette pass 2, [4] whole call.  Returns the number of stages written. */
 int phd_last_timings(double* ms, int n);
 
+/* Per-kernel GPU time from HIP events recorded on the launch stream around
+ * every launch of the kernels in `mask` (bit k = kernel k: 0 hsv_stats,
+ * 1 fft_rows, 2 fft_cols, 3 palette_cutoffs, 4 palette_sums, 5 sharpness).
+ * phd_profile_kernels resets the counters; phd_profile_read returns the
+ * accumulated milliseconds and launch count of one kernel. */
+int phd_profile_kernels(unsigned mask);
+int phd_profile_read(int kernel, double* total_ms, long* launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -152,7 +152,57 @@ const BlurTable* get_table(Context* c, int height, int width, int nr, int na) {
     return &(c->tables[key] = std::move(t));
 }
 
+int KernelProfiler::begin(int k, hipStream_t st) {
+    if (!(mask & (1u << k))) return -1;
+    const size_t slot = pending.size();
+    if (slot >= pool.size()) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return -1;
+        pool.emplace_back(a, b);
+    }
+    pending.push_back(k);
+    (void)hipEventRecord(pool[slot].first, st);
+    return (int)slot;
+}
+
+void KernelProfiler::end(int slot, hipStream_t st) {
+    if (slot >= 0) (void)hipEventRecord(pool[slot].second, st);
+}
+
+void KernelProfiler::collect() {
+    for (size_t i = 0; i < pending.size(); i++) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pool[i].first, pool[i].second) == hipSuccess) {
+            total_ms[pending[i]] += ms;
+            launches[pending[i]]++;
+        }
+    }
+    pending.clear();
+}
+
 }  // namespace phd
+
+extern "C" int phd_profile_kernels(unsigned mask) {
+    phd::Context* c = phd::get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->prof.mask = mask;
+    c->prof.pending.clear();
+    for (int k = 0; k < phd::kNumKernels; k++) {
+        c->prof.total_ms[k] = 0.0;
+        c->prof.launches[k] = 0;
+    }
+    return 0;
+}
+
+extern "C" int phd_profile_read(int kernel, double* total_ms, long* launches) {
+    phd::Context* c = phd::get_context();
+    if (!c || kernel < 0 || kernel >= phd::kNumKernels) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    *total_ms = c->prof.total_ms[kernel];
+    *launches = c->prof.launches[kernel];
+    return 0;
+}
 
 extern "C" const char* phd_last_error(void) { return phd::g_error.c_str(); }
 

@@ -70,6 +70,20 @@ struct FftPlanHost {
 };
 bool make_fft_plan(int n, FftPlanHost* p);
 
+// ---- per-kernel event timing (opt-in, phd_profile_kernels) -----------------
+enum KernelId { kK1 = 0, kFftRows = 1, kFftCols = 2, kCutoffs = 3, kPalSums = 4, kSharp = 5, kNumKernels = 6 };
+struct KernelProfiler {
+    unsigned mask = 0;                              // kernels to bracket with events
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    std::vector<int> pending;                       // kernel id per used pair
+    double total_ms[kNumKernels] = {};
+    long launches[kNumKernels] = {};
+    // record the opening event of a launch of kernel k (no-op unless enabled)
+    int begin(int k, hipStream_t st);
+    void end(int slot, hipStream_t st);
+    void collect();                                 // after the stream is drained
+};
+
 // ---- device context ---------------------------------------------------------
 struct Context {
     int device = -1;
@@ -87,6 +101,7 @@ struct Context {
     uint8_t* d_stage = nullptr;                    // upload staging for host images
     size_t stage_bytes = 0;
     hipEvent_t ev[8] = {};
+    KernelProfiler prof;
     std::mutex mu;
 };
 // The context of the current HIP device (created on first use).  nullptr if no GPU.

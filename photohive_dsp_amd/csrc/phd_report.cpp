@@ -270,7 +270,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         pd.hist = (unsigned*)(dw + L.A(i) + L.a_hist);
         pd.s_part = (double*)(dw + L.A(i) + L.a_spart);
         pd.chunk_hist = (unsigned short*)(dw + L.H(n, i));
+        const int ps = c->prof.begin(kK1, st);
         PHD_HIP(launch_hsv_stats(d_imgs[i], height, width, ds, gp, pd, nchunks, c->d_k255, st));
+        c->prof.end(ps, st);
     }
     PHD_HIP(hipEventRecord(c->ev[1], st));
     PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, st));
@@ -279,8 +281,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
         double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
         unsigned long long* fmx = (unsigned long long*)(dw + L.C(n, i) + L.c_fmax);
+        int ps = c->prof.begin(kFftRows, st);
         PHD_HIP(launch_fft_rows(d_imgs[i], height, width, prow->plan, sums, c->d_k255, c->d_inter, st));
+        c->prof.end(ps, st);
+        ps = c->prof.begin(kFftCols, st);
         PHD_HIP(launch_fft_cols(c->d_inter, height, wf, pcol->plan, tbl->d_map, nbins, bins, fmx, st));
+        c->prof.end(ps, st);
         if (ncrops) {
             // crop boxes: sharpness on the full-resolution luma before DC removal
             PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
@@ -313,18 +319,23 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         GroupRule* rules = (GroupRule*)(dw + L.B(n, i) + L.b_rules);
         const int* search = (const int*)(dw + L.B(n, i) + L.b_search);
         const double* off = (const double*)(dw + L.B(n, i) + L.b_off);
+        int ps = dec[i].search.empty() ? -1 : c->prof.begin(kCutoffs, st);
         PHD_HIP(launch_palette_cutoffs(d_imgs[i], height, width, ds, gp,
                                        (const unsigned short*)(dw + L.H(n, i)), nchunks, rules, search,
                                        (int)dec[i].search.size(), c->d_k255, st));
+        c->prof.end(ps, st);
+        ps = c->prof.begin(kPalSums, st);
         PHD_HIP(launch_palette_sums(d_imgs[i], height, width, ds, gp, rules, off,
                                     (int)dec[i].parents.size(), (double*)(dw + L.C(n, i) + L.c_pal),
                                     c->d_k255, st));
+        c->prof.end(ps, st);
     }
     PHD_HIP(hipEventRecord(c->ev[3], st));
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
     PHD_HIP(hipMemcpyAsync(hc, dw + L.C(n, 0), (size_t)n * L.c_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipEventRecord(c->ev[4], st));
     PHD_HIP(hipEventSynchronize(c->ev[4]));
+    c->prof.collect();
 
     int failures = 0;
     for (int i = 0; i < n; i++) {

@@ -65,6 +65,11 @@ lib.phd_fill_uniform_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes
 lib.phd_debug_hsv_groups_device.restype = ctypes.c_int
 lib.phd_debug_hsv_groups_device.argtypes = [ctypes.c_void_p, ctypes.c_long, P(PhdConfig), ctypes.c_void_p,
                                             ctypes.c_void_p]
+lib.phd_profile_kernels.restype = ctypes.c_int
+lib.phd_profile_kernels.argtypes = [ctypes.c_uint]
+lib.phd_profile_read.restype = ctypes.c_int
+lib.phd_profile_read.argtypes = [ctypes.c_int, P(ctypes.c_double), P(ctypes.c_long)]
+KERNELS = ["hsv_stats", "fft_rows", "fft_cols", "palette_cutoffs", "palette_sums", "sharpness"]
 lib.free_full_report.restype = None
 lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
 lib.phd_free_pgm.argtypes = [P(Image_PGM)]

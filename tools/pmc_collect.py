@@ -1,0 +1,78 @@
+"""Per-kernel HBM traffic from rocprofv3 PMC counters (run ON the GPU box).
+
+Two separate counter passes (FETCH_SIZE and WRITE_SIZE cannot share a pass on
+gfx950's TCC slots), each with only --pmc (no trace domains), over the same
+bench command.  Per MI355X_MICROARCH.md (HBM): bytes = counter * 1024, and
+FETCH_SIZE reads half the bytes of wide coalesced streaming reads on gfx950,
+so the read side is doubled.  Writes profiles/pmc_latest.json (+ a copy named
+by --tag) for bench.py's roofline.traffic.
+
+    python tools/pmc_collect.py --tag r01 -- --steps 2 --warmup 1 --batch 4
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHORT = {"k_hsv_stats": "hsv_stats", "k_fft_rows": "fft_rows", "k_fft_cols": "fft_cols",
+         "k_cutoffs": "palette_cutoffs", "k_palette_sums": "palette_sums", "k_sharp_pass": "sharpness"}
+
+
+def short(name):
+    for k, v in SHORT.items():
+        if k + "(" in name or name.endswith(k):
+            return v
+    return None
+
+
+def run_pass(counter, outdir, bench_args):
+    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
+           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-kernel-events"] + bench_args
+    subprocess.run(cmd, check=True, cwd=ROOT)
+    files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {outdir}")
+    per = {}
+    with open(files[0]) as f:
+        for row in csv.DictReader(f):
+            k = short(row.get("Kernel_Name", ""))
+            if not k or row.get("Counter_Name") != counter:
+                continue
+            per.setdefault(k, []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in per.items()}, files[0]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--tag", default="latest")
+    p.add_argument("--height", type=int, default=3000)
+    p.add_argument("--width", type=int, default=4000)
+    p.add_argument("rest", nargs=argparse.REMAINDER)
+    a = p.parse_args()
+    bench_args = [x for x in a.rest if x != "--"] + ["--height", str(a.height), "--width", str(a.width)]
+    out = os.path.join(ROOT, "gpurun_out", "pmc")
+    fetch, f1 = run_pass("FETCH_SIZE", out + "_fetch", bench_args)
+    write, f2 = run_pass("WRITE_SIZE", out + "_write", bench_args)
+    res = {"image": f"{a.height}x{a.width}", "source": [os.path.relpath(f1, ROOT), os.path.relpath(f2, ROOT)],
+           "correction": "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
+           "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        fb, wb = fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
+        res["kernels"][k] = {"fetch_size_kb": fetch.get(k), "write_size_kb": write.get(k),
+                             "hbm_bytes_per_launch": 2 * fb + wb}
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    # profiles/ for bench.py on this box; gpurun_out/ is what travels back
+    for d, name in ((os.path.join(ROOT, "profiles"), "pmc_latest.json"),
+                    (os.path.join(ROOT, "gpurun_out"), f"pmc_{a.tag}.json")):
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name), "w") as f:
+            json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
