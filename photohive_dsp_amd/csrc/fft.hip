@@ -8,7 +8,9 @@
 //  * Row pass: one block per PAIR of image rows.  Luma - avg of row y0 (real)
 //    and row y0+1 (imaginary) is built straight from the RGB8 bytes, one
 //    complex FFT of length W runs in LDS, and the two half spectra
-//    (W/2+1 bins each) are separated and written row-major to `inter`.
+//    (W/2+1 bins each) are separated and written COLUMN-major to `inter`
+//    ([W/2+1][H]): a column pass that gathers 16-32 B per row from a row-major
+//    spectrum ran at ~0.5 TB/s (ablation), a contiguous one streams.
 //  * Column pass: one block per C adjacent spectrum columns; C length-H FFTs
 //    in LDS, then the epilogue forms p = re*re + im*im, keeps a running max and
 //    accumulates log(p) for p >= 1 into the element's polar bin (LDS), so the
@@ -18,11 +20,11 @@
 // FFT engine: in-place Stockham autosort in LDS, every pass = all threads read
 // their butterflies' inputs into registers, barrier, write.  Twiddles come
 // from a host-built table tw[t] = exp(-2 pi i t/n) (long-double accurate).
+#include <cstdlib>
+
 #include "phd_device.h"
 
 namespace phd {
-
-constexpr int kFftThreads = 512;
 
 namespace {
 
@@ -101,162 +103,215 @@ __device__ __forceinline__ void butterfly<8>(double2 (&v)[8]) {
     }
 }
 
+// a / d for 0 <= a < 2^23 through one float multiply and an exact correction
+// (the float quotient is off by at most one at these magnitudes).
+__device__ __forceinline__ int fdiv(int a, int d, float inv) {
+    int q = (int)((float)a * inv);
+    const int r = a - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return q;
+}
+
+// W_n^e from the two LDS tables (e = 64*hi + lo).
+__device__ __forceinline__ double2 twiddle(const double2* lo, const double2* hi, int e) {
+    return cmul(hi[e >> 6], lo[e & 63]);
+}
+
 // One Stockham pass of radix R over `nseq` sequences of length n stored at
-// buf + seq*n (Govindaraju et al. formulation: read stride n/R, write
-// expanded index (j/Ns)*Ns*R + j%Ns + r*Ns).
-template <int R>
-__device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns, const double2* __restrict__ tw) {
-    constexpr int NB = (kFftMaxLds + R * kFftThreads - 1) / (R * kFftThreads);
+// buf + seq*n (Govindaraju et al.: read stride n/R, write expanded index
+// (j/Ns)*Ns*R + j%Ns + r*Ns).  Every thread reads its butterflies' inputs to
+// registers, applies w^r (w = W_n^{(j%Ns)*n/(Ns*R)}, powers by multiplication),
+// runs the radix-R DFT, then -- after one barrier -- writes them back.
+// CAP = elements per block the kernel instance supports (8 per thread).
+template <int R, int T>
+__device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns, const double2* lo,
+                                           const double2* hi) {
+    constexpr int NB = (8 * T + R * T - 1) / (R * T);
     const int nb = n / R, total = nb * nseq, tstep = n / (Ns * R);
+    const float inb = 1.0f / (float)nb, ins = 1.0f / (float)Ns;
     double2 v[NB][R];
+    int dst[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        const int t = threadIdx.x + b * kFftThreads;
+        const int t = threadIdx.x + b * T;
+        dst[b] = -1;
         if (t < total) {
-            const int seq = t / nb, j = t - seq * nb;
+            const int seq = nseq == 1 ? 0 : fdiv(t, nb, inb);
+            const int j = t - seq * nb;
             const double2* s = buf + seq * n;
 #pragma unroll
             for (int r = 0; r < R; r++) v[b][r] = s[j + r * nb];
-            const int jm = j % Ns;
+            const int jh = fdiv(j, Ns, ins), jm = j - jh * Ns;
             if (jm != 0) {
+                const double2 w = twiddle(lo, hi, jm * tstep);
+                double2 wr = w;
+                v[b][1] = cmul(v[b][1], w);
 #pragma unroll
-                for (int r = 1; r < R; r++) v[b][r] = cmul(v[b][r], tw[r * jm * tstep]);
+                for (int r = 2; r < R; r++) {
+                    wr = cmul(wr, w);
+                    v[b][r] = cmul(v[b][r], wr);
+                }
             }
             butterfly<R>(v[b]);
+            dst[b] = seq * n + jh * Ns * R + jm;
         }
     }
     __syncthreads();
 #pragma unroll
     for (int b = 0; b < NB; b++) {
-        const int t = threadIdx.x + b * kFftThreads;
-        if (t < total) {
-            const int seq = t / nb, j = t - seq * nb;
-            double2* s = buf + seq * n;
-            const int jm = j % Ns;
-            const int d = (j / Ns) * Ns * R + jm;
+        if (dst[b] >= 0) {
 #pragma unroll
-            for (int r = 0; r < R; r++) s[d + r * Ns] = v[b][r];
+            for (int r = 0; r < R; r++) buf[dst[b] + r * Ns] = v[b][r];
         }
     }
     __syncthreads();
 }
 
 // Generic radix (any R, incl. a prime length itself): output-parallel direct DFT.
-__device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns, int R, const double2* __restrict__ tw) {
-    constexpr int EG = kFftMaxLds / kFftThreads;   // outputs per thread (nseq*n <= kFftMaxLds)
+template <int T>
+__device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns, int R,
+                                          const double2* __restrict__ tw) {
+    constexpr int EG = 8;   // outputs per thread (nseq*n <= 8*T)
     const int nb = n / R, total = n * nseq, tstep = n / (Ns * R), nr = n / R;
     double2 out[EG];
+    int dst[EG];
 #pragma unroll
     for (int e = 0; e < EG; e++) {
-        const int t = threadIdx.x + e * kFftThreads;
+        const int t = threadIdx.x + e * T;
+        dst[e] = -1;
         if (t < total) {
             const int seq = t / n, rem = t - seq * n;
             const int j = rem / R, k = rem - j * R;       // butterfly j, output k
             const double2* s = buf + seq * n;
             const int jm = j % Ns;
-            const int step = jm * tstep + k * nr;         // twiddle exponent per input r (mod n)
+            const int step = (jm * tstep + k * nr) % n;   // twiddle exponent per input r (mod n)
             double2 acc = make_double2(0.0, 0.0);
             int ex = 0;
             for (int r = 0; r < R; r++) {
                 acc = cadd(acc, cmul(s[j + r * nb], tw[ex]));
                 ex += step;
-                if (ex >= n) ex -= n * (ex / n);
+                if (ex >= n) ex -= n;
             }
             out[e] = acc;
+            dst[e] = seq * n + (j / Ns) * Ns * R + jm + k * Ns;
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < EG; e++) {
-        const int t = threadIdx.x + e * kFftThreads;
-        if (t < total) {
-            const int seq = t / n, rem = t - seq * n;
-            const int j = rem / R, k = rem - j * R;
-            const int jm = j % Ns;
-            buf[seq * n + (j / Ns) * Ns * R + jm + k * Ns] = out[e];
-        }
-    }
+    for (int e = 0; e < EG; e++)
+        if (dst[e] >= 0) buf[dst[e]] = out[e];
     __syncthreads();
 }
 
-__device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan) {
+template <int T, bool GEN>
+__device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan, const double2* lo, const double2* hi) {
     int Ns = 1;
     for (int p = 0; p < plan.npass; p++) {
         const int R = plan.radix[p];
         switch (R) {
-            case 2: stockham_pass<2>(buf, plan.n, nseq, Ns, plan.tw); break;
-            case 3: stockham_pass<3>(buf, plan.n, nseq, Ns, plan.tw); break;
-            case 4: stockham_pass<4>(buf, plan.n, nseq, Ns, plan.tw); break;
-            case 5: stockham_pass<5>(buf, plan.n, nseq, Ns, plan.tw); break;
-            case 8: stockham_pass<8>(buf, plan.n, nseq, Ns, plan.tw); break;
-            default: generic_pass(buf, plan.n, nseq, Ns, R, plan.tw); break;
+            case 2: stockham_pass<2, T>(buf, plan.n, nseq, Ns, lo, hi); break;
+            case 3: stockham_pass<3, T>(buf, plan.n, nseq, Ns, lo, hi); break;
+            case 4: stockham_pass<4, T>(buf, plan.n, nseq, Ns, lo, hi); break;
+            case 5: stockham_pass<5, T>(buf, plan.n, nseq, Ns, lo, hi); break;
+            case 8: stockham_pass<8, T>(buf, plan.n, nseq, Ns, lo, hi); break;
+            default:
+                if constexpr (GEN) generic_pass<T>(buf, plan.n, nseq, Ns, R, plan.tw);
+                break;
         }
         Ns *= R;
     }
 }
 
-__global__ __launch_bounds__(kFftThreads) void k_fft_rows(const uint8_t* __restrict__ img, int H, int W,
-                                                          FftPlan plan,
-                                                          const unsigned long long* __restrict__ sums,
-                                                          const double* __restrict__ k255g,
-                                                          double2* __restrict__ inter) {
+// Stage the two twiddle tables in LDS at `tw` (64 + n_hi entries).
+__device__ __forceinline__ void load_twiddles(double2* tw, const FftPlan& plan) {
+    for (int i = threadIdx.x; i < 64 + plan.n_hi; i += blockDim.x)
+        tw[i] = i < 64 ? plan.tw_lo[i] : plan.tw_hi[i - 64];
+}
+
+// LDS: [ W complex | twiddles (64 + n_hi) | k255 (256 doubles) ]
+template <int T, bool GEN>
+__global__ __launch_bounds__(T) void k_fft_rows(const uint8_t* __restrict__ img, int H, int W, FftPlan plan,
+                                                const unsigned long long* __restrict__ sums,
+                                                const double* __restrict__ k255g, double2* __restrict__ inter) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
-    double* k255 = reinterpret_cast<double*>(smem + sizeof(double2) * W);
+    double2* tw = buf + W;
+    double* k255 = reinterpret_cast<double*>(tw + 64 + plan.n_hi);
     const int tid = threadIdx.x;
     if (tid < 256) k255[tid] = k255g[tid];
+    load_twiddles(tw, plan);
     // avg = (Br + Bg + Bb) / 3 (src/interface.c:78) from the exact integer sums
     const double n = (double)H * (double)W;
     const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
                         (double)sums[2] / 255.0 / n) / 3.0;
     __syncthreads();
-    const int y0 = 2 * blockIdx.x, y1 = y0 + 1;
+    // XCD-aware order: 4 consecutive row pairs (8 rows = one 128-byte line of
+    // each column of the column-major output) run back to back on one XCD so
+    // their 32-byte partial-line writes merge in that XCD's L2.
+    int pb = blockIdx.x;
+    {
+        const int group = 32;                       // 8 XCD slots x 4 pairs
+        const int full = (int)(gridDim.x / group) * group;
+        if (pb < full) {
+            const int x = pb % 8, t = pb / 8;
+            pb = (t / 4) * group + x * 4 + (t % 4);
+        }
+    }
+    const int y0 = 2 * pb, y1 = y0 + 1;
     const bool two = y1 < H;
     const uint8_t* r0 = img + (size_t)y0 * W * 3;
     const uint8_t* r1 = img + (size_t)(two ? y1 : y0) * W * 3;
-    for (int x = tid; x < W; x += kFftThreads) {
+    for (int x = tid; x < W; x += T) {
         // rgb2pgm (image_processing.c:509), then remove_dc_bias (blur_profile.c:236)
         const double p0 = 0.299 * k255[r0[3 * x]] + 0.587 * k255[r0[3 * x + 1]] + 0.114 * k255[r0[3 * x + 2]];
         const double p1 = 0.299 * k255[r1[3 * x]] + 0.587 * k255[r1[3 * x + 1]] + 0.114 * k255[r1[3 * x + 2]];
         buf[x] = make_double2(p0 - avg, two ? p1 - avg : 0.0);
     }
     __syncthreads();
-    fft_lds(buf, 1, plan);
+    fft_lds<T, GEN>(buf, 1, plan, tw, tw + 64);
     // Z = A + iB with A, B the spectra of the two real rows:
     // A[k] = (Z[k] + conj Z[W-k]) / 2, B[k] = (Z[k] - conj Z[W-k]) / (2i)
+    // written column-major, inter[k][y] (ld = H): lane pairs cover (k, y0), (k, y1)
     const int wf = W / 2 + 1;
-    double2* o0 = inter + (size_t)y0 * wf;
-    double2* o1 = inter + (size_t)y1 * wf;
-    for (int k = tid; k < wf; k += kFftThreads) {
+    for (int i = tid; i < 2 * wf; i += T) {
+        const int k = i >> 1, second = i & 1;
+        if (second && !two) continue;
         const double2 zk = buf[k], zm = buf[k == 0 ? 0 : W - k];
-        o0[k] = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-        if (two) o1[k] = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+        inter[(size_t)k * H + y0 + second] =
+            second ? make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x))
+                   : make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
     }
 }
 
-__global__ __launch_bounds__(kFftThreads) void k_fft_cols(const double2* __restrict__ inter, int H, int wf,
-                                                          int C, FftPlan plan,
-                                                          const uint16_t* __restrict__ binmap, int nbins,
-                                                          int lds_bins, double* __restrict__ bin_sums,
-                                                          unsigned long long* __restrict__ fmax_bits) {
+// LDS: [ C*H complex | twiddles (64 + n_hi) | polar bins (nbins doubles, if lds_bins) ]
+template <int T, bool GEN>
+__global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inter, int H, int wf, int C,
+                                                FftPlan plan, const uint16_t* __restrict__ binmap, int nbins,
+                                                int lds_bins, double* __restrict__ bin_sums,
+                                                double* __restrict__ fmax_part, int ablate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
+    double2* tw = buf + (size_t)C * H;
+    double* lb = reinterpret_cast<double*>(tw + 64 + plan.n_hi);
     const int tid = threadIdx.x;
-    const int k0 = blockIdx.x * C;
+    const int cb = blockIdx.x;
+    const int k0 = cb * C;
     const int nc = min(C, wf - k0);
-    double* lb = reinterpret_cast<double*>(smem + sizeof(double2) * (size_t)C * H);
+    load_twiddles(tw, plan);
     if (lds_bins)
-        for (int i = tid; i < nbins; i += kFftThreads) lb[i] = 0.0;
-    for (int i = tid; i < nc * H; i += kFftThreads) {
-        const int y = i / nc, c = i - y * nc;
-        buf[c * H + y] = inter[(size_t)y * wf + k0 + c];
+        for (int i = tid; i < nbins; i += T) lb[i] = 0.0;
+    {
+        // the nc columns are one contiguous run of the column-major spectrum
+        const double2* src = inter + (size_t)k0 * H;
+        for (int i = tid; i < nc * H; i += T) buf[i] = src[i];
     }
     __syncthreads();
-    fft_lds(buf, nc, plan);
+    if (!(ablate & 1)) fft_lds<T, GEN>(buf, nc, plan, tw, tw + 64);
     double mx = 0.0;
     double* acc = lds_bins ? lb : bin_sums;
-    const int total = nc * H;
-    for (int i0 = 0; i0 < total; i0 += kFftThreads) {
+    const int total = (ablate & 2) ? 0 : nc * H;
+    for (int i0 = 0; i0 < total; i0 += T) {
         const int i = i0 + tid;
         int b = -1;
         double lg = 0.0;
@@ -278,11 +333,20 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_cols(const double2* __restr
             atomicAdd(&acc[b], lg);
         }
     }
+    // block max -> one partial per block (a per-wave atomicMax on one word
+    // serialised ~16K atomics per image: ~160 us, DESIGN.md ablation)
     mx = wave_max(mx);
-    if (lane_id() == 0) atomicMax(fmax_bits, (unsigned long long)__double_as_longlong(mx));
-    if (lds_bins) {
-        __syncthreads();
-        for (int i = tid; i < nbins; i += kFftThreads) {
+    __syncthreads();                      // buf is free now: reuse it as scratch
+    double* red = reinterpret_cast<double*>(buf);
+    if (lane_id() == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        double m = 0.0;
+        for (int w = 0; w < T / 64; w++) m = fmax(m, red[w]);
+        fmax_part[blockIdx.x] = m;
+    }
+    if (lds_bins && !(ablate & 4)) {
+        for (int i = tid; i < nbins; i += T) {
             const double a = lb[i];
             if (a != 0.0) atomicAdd(&bin_sums[i], a);
         }
@@ -291,43 +355,70 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_cols(const double2* __restr
 
 }  // namespace
 
-// Kernels here may use up to the full 160 KiB LDS of a gfx950 CU.
-static void allow_big_lds() {
-    static bool done = false;
-    if (done) return;
-    done = true;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fft_rows),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fft_cols),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+template <typename K>
+static void allow_big_lds(K kernel) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
+template <int T, bool GEN>
+static hipError_t rows_impl(const uint8_t* img, int height, int width, const FftPlan& plan,
+                            const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st) {
+    static bool once = (allow_big_lds(k_fft_rows<T, GEN>), true);
+    (void)once;
+    const size_t lds = sizeof(double2) * (width + 64 + plan.n_hi) + 256 * sizeof(double);
+    hipLaunchKernelGGL((k_fft_rows<T, GEN>), dim3((height + 1) / 2), dim3(T), lds, st, img, height, width, plan,
+                       sums, k255, inter);
+    return hipGetLastError();
 }
 
 hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftPlan& plan,
                            const unsigned long long* sums, const double* k255, double2* inter,
                            hipStream_t st) {
-    allow_big_lds();
-    const size_t lds = sizeof(double2) * width + 256 * sizeof(double);
-    hipLaunchKernelGGL(k_fft_rows, dim3((height + 1) / 2), dim3(kFftThreads), lds, st, img, height,
-                       width, plan, sums, k255, inter);
+    if (width <= 4096)
+        return plan.generic ? rows_impl<512, true>(img, height, width, plan, sums, k255, inter, st)
+                            : rows_impl<512, false>(img, height, width, plan, sums, k255, inter, st);
+    return plan.generic ? rows_impl<1024, true>(img, height, width, plan, sums, k255, inter, st)
+                        : rows_impl<1024, false>(img, height, width, plan, sums, k255, inter, st);
+}
+
+template <int T, bool GEN>
+static hipError_t cols_impl(const double2* inter, int height, int wf, int C, const FftPlan& plan,
+                            const uint16_t* binmap, int nbins, int lds_bins, size_t lds, double* bin_sums,
+                            double* fmax_part, hipStream_t st) {
+    static bool once = (allow_big_lds(k_fft_cols<T, GEN>), true);
+    (void)once;
+    static const int ablate = getenv("PHD_ABLATE") ? atoi(getenv("PHD_ABLATE")) : 0;   // debug only
+    hipLaunchKernelGGL((k_fft_cols<T, GEN>), dim3((wf + C - 1) / C), dim3(T), lds, st, inter, height, wf, C, plan,
+                       binmap, nbins, lds_bins, bin_sums, fmax_part, ablate);
     return hipGetLastError();
+}
+
+int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds_out, int* lds_bins_out) {
+    constexpr size_t kLdsBudget = 158 * 1024;
+    const size_t bins_bytes = sizeof(double) * nbins;
+    const int lds_bins = bins_bytes <= 48 * 1024;
+    const size_t fixed = sizeof(double2) * (64 + plan.n_hi) + (lds_bins ? bins_bytes : 0);
+    const size_t col_bytes = sizeof(double2) * height;
+    int C = 1;
+    while (C < 8 && (size_t)(2 * C) * height <= (size_t)kFftMaxLds && (2 * C) * col_bytes + fixed <= kLdsBudget)
+        C *= 2;
+    if (lds_out) *lds_out = C * col_bytes + fixed;
+    if (lds_bins_out) *lds_bins_out = lds_bins;
+    return C;
 }
 
 hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
                            const uint16_t* binmap, int nbins, double* bin_sums,
-                           unsigned long long* fmax_bits, hipStream_t st) {
-    allow_big_lds();
-    constexpr size_t kLdsBudget = 152 * 1024;
-    const size_t bins_bytes = sizeof(double) * nbins;
-    const int lds_bins = bins_bytes <= 48 * 1024;
-    const size_t col_bytes = sizeof(double2) * height;
-    int C = 1;
-    while (C < 8 && (size_t)(2 * C) * height <= (size_t)kFftMaxLds &&
-           (2 * C) * col_bytes + (lds_bins ? bins_bytes : 0) <= kLdsBudget)
-        C *= 2;
-    const size_t lds = C * col_bytes + (lds_bins ? bins_bytes : 0);
-    hipLaunchKernelGGL(k_fft_cols, dim3((wf + C - 1) / C), dim3(kFftThreads), lds, st, inter, height,
-                       wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_bits);
-    return hipGetLastError();
+                           double* fmax_part, hipStream_t st) {
+    size_t lds;
+    int lds_bins;
+    const int C = fft_cols_blocks(height, wf, nbins, plan, &lds, &lds_bins);
+    if ((size_t)C * height <= 4096)
+        return plan.generic ? cols_impl<512, true>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st)
+                            : cols_impl<512, false>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st);
+    return plan.generic ? cols_impl<1024, true>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st)
+                        : cols_impl<1024, false>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st);
 }
 
 }  // namespace phd

@@ -120,18 +120,29 @@ bool make_fft_plan(int n, FftPlanHost* p) {
         set_error("FFT length " + std::to_string(n) + " has too many factors");
         return false;
     }
-    std::vector<double2> tw(n);
-    const long double two_pi = 6.283185307179586476925286766559005768L;
-    for (int t = 0; t < n; t++) {
-        const long double a = two_pi * (long double)t / (long double)n;
-        tw[t] = make_double2((double)cosl(a), (double)-sinl(a));
+    P.generic = 0;
+    for (int i = 0; i < P.npass; i++) {
+        const int r = P.radix[i];
+        if (r != 2 && r != 3 && r != 4 && r != 5 && r != 8) P.generic = 1;
     }
-    if (hipMalloc(&p->d_tw, sizeof(double2) * n) != hipSuccess ||
-        hipMemcpy(p->d_tw, tw.data(), sizeof(double2) * n, hipMemcpyHostToDevice) != hipSuccess) {
+    P.n_hi = (n + 63) / 64;
+    const long double two_pi = 6.283185307179586476925286766559005768L;
+    auto w = [&](long t) {
+        const long double a = two_pi * (long double)(t % n) / (long double)n;
+        return make_double2((double)cosl(a), (double)-sinl(a));
+    };
+    std::vector<double2> tw(n + 64 + P.n_hi);
+    for (int t = 0; t < n; t++) tw[t] = w(t);
+    for (int t = 0; t < 64; t++) tw[n + t] = w(t);
+    for (int t = 0; t < P.n_hi; t++) tw[n + 64 + t] = w(64L * t);
+    if (hipMalloc(&p->d_tw, sizeof(double2) * tw.size()) != hipSuccess ||
+        hipMemcpy(p->d_tw, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice) != hipSuccess) {
         set_error("twiddle upload failed");
         return false;
     }
     P.tw = p->d_tw;
+    P.tw_lo = p->d_tw + n;
+    P.tw_hi = p->d_tw + n + 64;
     return true;
 }
 

@@ -41,12 +41,18 @@ struct GroupRule {
     unsigned last;       // raster index of the group's last pixel (filled on device)
 };
 
-// A mixed-radix FFT plan for one length (radix sequence + twiddle table).
+// A mixed-radix FFT plan for one length.  Twiddles W_n^e = exp(-2 pi i e/n)
+// come from two small tables (e = 64*hi + lo) that each block stages in LDS;
+// the full table is only used by the generic-radix pass.
 struct FftPlan {
     int n;
     int npass;
+    int generic;               // some radix is outside {2,3,4,5,8}
+    int n_hi;                  // entries of tw_hi = ceil(n / 64)
     int radix[kMaxFftPasses];
-    const double2* tw;   // device: tw[t] = exp(-2 pi i t / n), t in [0, n)
+    const double2* tw;         // device: tw[t] = W_n^t, t in [0, n)
+    const double2* tw_lo;      // device: W_n^t, t in [0, 64)
+    const double2* tw_hi;      // device: W_n^(64 t), t in [0, n_hi)
 };
 
 // ---- launchers (kernels in *.hip) ------------------------------------------
@@ -65,16 +71,18 @@ hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds
                                const double* slot_off, int nslots, double* out,
                                const double* k255, hipStream_t st);
 // Row pass: luma - avg of two rows as one complex sequence, FFT, split, write
-// the half spectra row-major into inter[height][wf].
+// the half spectra column-major into inter[wf][height].
 hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftPlan& plan,
                            const unsigned long long* sums, const double* k255,
                            double2* inter, hipStream_t st);
 // Column pass + epilogue: power, running max, sum log(p) over p >= 1 per
 // polar bin (binmap[wf][height], uint16 bin ids).  Accumulates into
-// bin_sums[na*nr] (fp64) and fmax_bits (max power as uint64 bits).
+// bin_sums[na*nr] (fp64) and writes one max power per block to fmax_part.
 hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
                            const uint16_t* binmap, int nbins, double* bin_sums,
-                           unsigned long long* fmax_bits, hipStream_t st);
+                           double* fmax_part, hipStream_t st);
+// Column blocks of launch_fft_cols (= entries of fmax_part); optional LDS size.
+int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds, int* lds_bins);
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const double* k255, int* gid,
                             double* hsv, hipStream_t st);
 hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st);

@@ -41,7 +41,7 @@ struct Layout {
     size_t H(int n, int i) const { return (size_t)n * (a_bytes + c_bytes + b_bytes) + (size_t)i * chunk_bytes; }
 };
 
-Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops) {
+Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolblocks) {
     Layout L{};
     L.a_sums = 0;
     L.a_hist = al(6 * sizeof(unsigned long long));
@@ -49,7 +49,7 @@ Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops) {
     L.a_bytes = L.a_spart + al(sizeof(double) * nchunks);
     L.c_bins = 0;
     L.c_fmax = al(sizeof(double) * nbins);
-    L.c_pal = L.c_fmax + al(sizeof(unsigned long long));
+    L.c_pal = L.c_fmax + al(sizeof(double) * (ncolblocks > 0 ? ncolblocks : 1));
     L.c_sharp = L.c_pal + al(sizeof(double) * 4 * tl);
     L.c_bytes = L.c_sharp + al(sizeof(double) * 2 * (ncrops > 0 ? ncrops : 1));
     L.b_rules = 0;
@@ -245,7 +245,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
     if (!prow || !pcol || !tbl) return false;
 
-    const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops);
+    const int C = fft_cols_blocks(height, wf, nbins, pcol->plan, nullptr, nullptr);
+    const int ncolblocks = (wf + C - 1) / C;
+    const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, sizeof(double2) * (size_t)height * wf))
         return false;
@@ -280,7 +282,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     for (int i = 0; i < n; i++) {
         const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
         double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
-        unsigned long long* fmx = (unsigned long long*)(dw + L.C(n, i) + L.c_fmax);
+        double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
         int ps = c->prof.begin(kFftRows, st);
         PHD_HIP(launch_fft_rows(d_imgs[i], height, width, prow->plan, sums, c->d_k255, c->d_inter, st));
         c->prof.end(ps, st);
@@ -350,10 +352,10 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         double s_acc = 0.0;
         for (int k = 0; k < nchunks; k++) s_acc += spart[k];
         const RGB_Statistics st_i = stats_from_sums(sums, (long)height * width);
-        unsigned long long fbits;
-        memcpy(&fbits, cc + L.c_fmax, sizeof(fbits));
-        double fmax;
-        memcpy(&fmax, &fbits, sizeof(fmax));
+        // pgm_normalize_fft's max (src/fft_processing.c:181-184) over the block partials
+        const double* fpart = (const double*)(cc + L.c_fmax);
+        double fmax = 0.0;
+        for (int b = 0; b < ncolblocks; b++) fmax = fpart[b] > fmax ? fpart[b] : fmax;
         std::string w;
         out[i] = assemble(st_i, s_acc / (double)n_hsv, dec[i], (const double*)(cc + L.c_pal), n_hsv, *tbl,
                           (const double*)(cc + L.c_bins), fmax, cfg, crops,
@@ -386,7 +388,7 @@ bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, 
     const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
     const long n_hsv = hsv_count(height, width, ds);
     const int nchunks = (int)((n_hsv + kChunk - 1) / kChunk);
-    const Layout L = make_layout(1, gp.tl, nchunks, 1, 0);
+    const Layout L = make_layout(1, gp.tl, nchunks, 1, 0, 1);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total)) return false;
     uint8_t* dw = (uint8_t*)c->d_ws;
     uint8_t* hp = (uint8_t*)c->h_pin;
