@@ -170,6 +170,12 @@ int phd_fill_uniform_device(uint8_t* d_dst, size_t n, uint64_t seed, void* strea
 int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, const phd_config* cfg, int* d_gid,
                                 double* d_hsv);
 
+/* Micro-benchmark hook: average ms per launch of one pipeline kernel (0 hsv_stats,
+ * 1 fft_rows, 2 fft_cols) over `iters` launches on a device image; `ablate` is a
+ * debug mask (0 = production kernel). */
+int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int height, int width, const phd_config* cfg,
+                          int ablate, int iters, double* avg_ms);
+
 /* Free an Image_PGM returned by get_blur_profile_visual. */
 void phd_free_pgm(Image_PGM* img);
 

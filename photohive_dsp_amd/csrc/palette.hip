@@ -11,6 +11,8 @@
 // Layout: one image = interleaved RGB8, row-major, 3*W bytes per row.  A block
 // owns kChunk consecutive hsv pixels; each thread consumes 4 consecutive pixels
 // (12 bytes, one dwordx3 load) per step so a wave reads 768 contiguous bytes.
+#include <cstdlib>
+
 #include "phd_device.h"
 
 namespace phd {
@@ -18,19 +20,34 @@ namespace phd {
 namespace {
 
 // LDS carve of K1 (one dynamic array, 16-B aligned base: no static __shared__).
+constexpr int kQueue = kChunk;               // deferred exact-path pixels (u16 offsets): never overflows
+constexpr int kK1Threads = 1024;             // K1 block: 16 waves over one kChunk
 struct K1Lds {
     static constexpr int k255 = 0;           // 256 doubles
-    static constexpr int red = 2048;         // 4 waves x 8 x u64
-    static constexpr int hist = 2048 + 256;  // tl x u32
+    static constexpr int rinv = 2048;        // 256 doubles
+    static constexpr int vcol = 4096;        // 256 int16
+    static constexpr int vgray = 4608;       // 256 int16
+    static constexpr int red = 5120;         // 16 waves x 8 x u64
+    static constexpr int qn = 6144;          // int (+pad)
+    static constexpr int queue = 6160;       // kQueue x u16 (pixel offset in the chunk)
+    static constexpr int hist = 6160 + 2 * kQueue;   // tl x u32
 };
+
+__device__ __forceinline__ void stage_tables(unsigned char* smem, const double* __restrict__ k255g,
+                                             const ClassTables* __restrict__ tabs) {
+    const int tid = threadIdx.x;
+    if (tid >= 256) return;
+    reinterpret_cast<double*>(smem + K1Lds::k255)[tid] = k255g[tid];
+    reinterpret_cast<double*>(smem + K1Lds::rinv)[tid] = tabs->rinv[tid];
+    reinterpret_cast<short*>(smem + K1Lds::vcol)[tid] = tabs->vcol[tid];
+    reinterpret_cast<short*>(smem + K1Lds::vgray)[tid] = tabs->vgray[tid];
+}
 
 __device__ __forceinline__ void load4(const uint8_t* __restrict__ img, long p0, long end,
                                       bool aligned, unsigned (&k)[12], int& nvalid) {
     if (aligned && p0 + 3 < end) {
         const unsigned* w = reinterpret_cast<const unsigned*>(img + 3 * p0);
-        const unsigned w0 = __builtin_nontemporal_load(w + 0);
-        const unsigned w1 = __builtin_nontemporal_load(w + 1);
-        const unsigned w2 = __builtin_nontemporal_load(w + 2);
+        const unsigned w0 = w[0], w1 = w[1], w2 = w[2];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             k[i] = (w0 >> (8 * i)) & 255u;
@@ -54,6 +71,29 @@ __device__ __forceinline__ void load4(const uint8_t* __restrict__ img, long p0, 
     }
 }
 
+// Raw form of load4: the three little-endian words holding pixels p0..p0+3
+// (bytes past `end` are zero); unpack with px_byte.
+__device__ __forceinline__ int load4_raw(const uint8_t* __restrict__ img, long p0, long end, bool aligned,
+                                         unsigned (&w)[3]) {
+    if (aligned && p0 + 3 < end) {
+        const unsigned* q = reinterpret_cast<const unsigned*>(img + 3 * p0);
+        w[0] = q[0];
+        w[1] = q[1];
+        w[2] = q[2];
+        return 4;
+    }
+    w[0] = w[1] = w[2] = 0;
+    int nv = 0;
+    for (int b = 0; b < 12; b++)
+        if (p0 + b / 3 < end) {
+            w[b >> 2] |= (unsigned)img[3 * p0 + b] << (8 * (b & 3));
+            nv = b / 3 + 1;
+        }
+    return nv;
+}
+
+__device__ __forceinline__ int px_byte(const unsigned (&w)[3], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255; }
+
 // Add one to lds[g] for every lane with g >= 0; a wave whose lanes all hit the
 // same group issues one atomic (flat regions of real images).
 __device__ __forceinline__ void hist_add(unsigned* lds, int g) {
@@ -67,91 +107,132 @@ __device__ __forceinline__ void hist_add(unsigned* lds, int g) {
 }
 
 // K1 for downsample_rate == 1: stats and HSV over the same pixels.
-__global__ __launch_bounds__(kThreads) void k_hsv_stats(const uint8_t* __restrict__ img, long npix,
-                                                        GridParams gp, const double* __restrict__ k255g,
-                                                        int aligned, PaletteDev out) {
+// Persistent blocks (2 per CU) walk the image's kChunk-pixel chunks; per chunk
+// the group histogram is built in LDS and written out (the cutoff search walks
+// these per-chunk counts); channel moments and sum(s) stay in registers and are
+// reduced once per block.  Pixels classify through fast_group; the few near a
+// bin edge are queued in LDS and classified exactly after the chunk's stream,
+// so waves stay convergent.  Next-chunk loads are issued before the current
+// chunk's flush.
+__global__ __launch_bounds__(kK1Threads, 8) void k_hsv_stats(const uint8_t* __restrict__ img, long npix,
+                                                        int nchunks, GridParams gp, FastCls fc,
+                                                        const ClassTables* __restrict__ tabs,
+                                                        const double* __restrict__ k255g,
+                                                        int aligned, PaletteDev out, int ablate) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* k255 = reinterpret_cast<double*>(smem + K1Lds::k255);
+    const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
+    const double* rinv = reinterpret_cast<const double*>(smem + K1Lds::rinv);
+    const short* vcol = reinterpret_cast<const short*>(smem + K1Lds::vcol);
+    const short* vgray = reinterpret_cast<const short*>(smem + K1Lds::vgray);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + K1Lds::red);
+    int* qn = reinterpret_cast<int*>(smem + K1Lds::qn);
+    unsigned short* queue = reinterpret_cast<unsigned short*>(smem + K1Lds::queue);
     unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);
     const int tid = threadIdx.x;
-    k255[tid] = k255g[tid];
-    for (int i = tid; i < gp.tl; i += kThreads) lh[i] = 0;
-    __syncthreads();
-
-    const long base = (long)blockIdx.x * kChunk;
-    const long end = min(base + (long)kChunk, npix);
-    unsigned sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
+    stage_tables(smem, k255g, tabs);
+    unsigned long long mom[6] = {0, 0, 0, 0, 0, 0};
     double ssum = 0.0;
-    for (long p0 = base + 4L * tid; p0 < end; p0 += 4L * kThreads) {
-        unsigned k[12];
-        int nv;
-        load4(img, p0, end, aligned != 0, k, nv);
+    constexpr int kSteps = kChunk / (4 * kK1Threads);
+    unsigned w[kSteps][3];
+    int nv[kSteps];
+    auto issue = [&](int c) {
+        const long base = (long)c * kChunk, end = min(base + (long)kChunk, npix);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const unsigned kr = k[3 * i], kg = k[3 * i + 1], kb = k[3 * i + 2];
-            sr += kr; sg += kg; sb += kb;
-            qr += kr * kr; qg += kg * kg; qb += kb * kb;
-            double h, s, v;
-            rgb2hsv(k255[kr], k255[kg], k255[kb], h, s, v);
-            const bool valid = i < nv;
-            ssum += valid ? s : 0.0;
-            hist_add(lh, valid ? group_of(gp, h, s, v) : -1);
+        for (int it = 0; it < kSteps; it++)
+            nv[it] = load4_raw(img, base + 4L * tid + 4L * kK1Threads * it, end, aligned != 0, w[it]);
+    };
+    int c = blockIdx.x;
+    if (c < nchunks) issue(c);
+    for (; c < nchunks; c += gridDim.x) {
+        for (int i = tid; i < gp.tl; i += kK1Threads) lh[i] = 0;
+        if (tid == 0) *qn = 0;
+        __syncthreads();
+        const long base = (long)c * kChunk;
+        unsigned sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
+#pragma unroll
+        for (int it = 0; it < kSteps; it++) {
+            const long p0 = base + 4L * tid + 4L * kK1Threads * it;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int kr = px_byte(w[it], 3 * i), kg = px_byte(w[it], 3 * i + 1), kb = px_byte(w[it], 3 * i + 2);
+                const bool valid = i < nv[it];
+                if (valid) {
+                    sr += kr; sg += kg; sb += kb;
+                    qr += kr * kr; qg += kg * kg; qb += kb * kb;
+                }
+                if (!(ablate & 32)) ssum += valid ? sat_of(kr, kg, kb, rinv) : 0.0;
+                int g = !valid ? -1 : (ablate & 8) ? (kr & 7) : fast_group(kr, kg, kb, vcol, vgray, gp, fc);
+                if (g == -2) {                // near a bin edge: classify exactly after the stream
+                    queue[atomicAdd(qn, 1)] = (unsigned short)(p0 + i - base);
+                    g = -1;
+                }
+                if (!(ablate & 16)) hist_add(lh, g);
+                else if (g >= 0) ssum += g;
+            }
         }
+        mom[0] += sr; mom[1] += sg; mom[2] += sb; mom[3] += qr; mom[4] += qg; mom[5] += qb;
+        if (c + (int)gridDim.x < nchunks) issue(c + gridDim.x);   // prefetch the next chunk
+        __syncthreads();
+        const int nq = *qn;
+        for (int q = tid; q < nq; q += kK1Threads) {
+            const long p = base + queue[q];
+            atomicAdd(&lh[exact_group(img[3 * p], img[3 * p + 1], img[3 * p + 2], k255, gp)], 1u);
+        }
+        __syncthreads();
+        for (int i = tid; i < gp.tl; i += kK1Threads) {
+            const unsigned n = lh[i];
+            out.chunk_hist[(long)c * gp.tl + i] = (unsigned short)n;
+            if (n && !(ablate & 128)) atomicAdd(&out.hist[i], n);
+        }
+        __syncthreads();
     }
-    // block reduction of the integer moments (exact) and of sum(s)
-    unsigned long long m[6] = {sr, sg, sb, qr, qg, qb};
-    const int w = tid >> 6;
+    // block reduction of the integer moments (exact) and of sum(s), once
+    const int wv = tid >> 6;
 #pragma unroll
-    for (int c = 0; c < 6; c++) m[c] = wave_sum(m[c]);
+    for (int k = 0; k < 6; k++) mom[k] = wave_sum(mom[k]);
     const double sw = wave_sum(ssum);
     if (lane_id() == 0) {
 #pragma unroll
-        for (int c = 0; c < 6; c++) red[w * 8 + c] = m[c];
-        reinterpret_cast<double*>(red)[w * 8 + 6] = sw;
+        for (int k = 0; k < 6; k++) red[wv * 8 + k] = mom[k];
+        reinterpret_cast<double*>(red)[wv * 8 + 6] = sw;
     }
     __syncthreads();
     if (tid < 6) {
         unsigned long long t = 0;
-        for (int q = 0; q < kThreads / 64; q++) t += red[q * 8 + tid];
-        atomicAdd(&out.sums[tid], t);
+        for (int q = 0; q < kK1Threads / 64; q++) t += red[q * 8 + tid];
+        if (!(ablate & 128)) atomicAdd(&out.sums[tid], t);
     } else if (tid == 6) {
         double t = 0.0;
-        for (int q = 0; q < kThreads / 64; q++) t += reinterpret_cast<double*>(red)[q * 8 + 6];
-        out.s_part[blockIdx.x] = t;
-    }
-    for (int i = tid; i < gp.tl; i += kThreads) {
-        const unsigned c = lh[i];
-        out.chunk_hist[(long)blockIdx.x * gp.tl + i] = (unsigned short)c;
-        if (c) atomicAdd(&out.hist[i], c);
+        for (int q = 0; q < kK1Threads / 64; q++) t += reinterpret_cast<double*>(red)[q * 8 + 6];
+        out.s_part[blockIdx.x] = t;        // one partial per block (host sums them)
     }
 }
 
 // K1 for downsample_rate > 1: HSV over the decimated pixels only (gathered).
 __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__ img, long npix,
-                                                     int width, int ds, int nw, GridParams gp,
-                                                     const double* __restrict__ k255g,
-                                                     PaletteDev out) {
+                                                     int width, int ds, int nw, GridParams gp, FastCls fc,
+                                                     const ClassTables* __restrict__ tabs,
+                                                     const double* __restrict__ k255g, PaletteDev out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double* k255 = reinterpret_cast<double*>(smem + K1Lds::k255);
+    const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
+    const double* rinv = reinterpret_cast<const double*>(smem + K1Lds::rinv);
+    const short* vcol = reinterpret_cast<const short*>(smem + K1Lds::vcol);
+    const short* vgray = reinterpret_cast<const short*>(smem + K1Lds::vgray);
     double* red = reinterpret_cast<double*>(smem + K1Lds::red);
     unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);
     const int tid = threadIdx.x;
-    k255[tid] = k255g[tid];
+    stage_tables(smem, k255g, tabs);
     for (int i = tid; i < gp.tl; i += kThreads) lh[i] = 0;
     __syncthreads();
     const long base = (long)blockIdx.x * kChunk;
     const long end = min(base + (long)kChunk, npix);
     double ssum = 0.0;
-    for (long j = base + tid; j < end + ((end - base) % kThreads ? kThreads : 0); j += kThreads) {
-        int g = -1;
-        if (j < end) {
-            const long p = src_pixel(j, width, ds, nw);
-            double h, s, v;
-            rgb2hsv(k255[img[3 * p]], k255[img[3 * p + 1]], k255[img[3 * p + 2]], h, s, v);
-            ssum += s;
-            g = group_of(gp, h, s, v);
-        }
+    for (long j = base + tid; j < end; j += kThreads) {
+        const long p = src_pixel(j, width, ds, nw);
+        const int kr = img[3 * p], kg = img[3 * p + 1], kb = img[3 * p + 2];
+        ssum += sat_of(kr, kg, kb, rinv);
+        int g = fast_group(kr, kg, kb, vcol, vgray, gp, fc);
+        if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
         hist_add(lh, g);
     }
     const double sw = wave_sum(ssum);
@@ -378,15 +459,19 @@ __global__ __launch_bounds__(kThreads) void k_palette_sums(const uint8_t* __rest
     }
 }
 
-// Per-pixel HSV and group id (validation of the device arithmetic).
-__global__ void k_debug_hsv(const uint8_t* __restrict__ img, long n, GridParams gp,
-                            const double* __restrict__ k255, int* __restrict__ gid,
-                            double* __restrict__ hsv) {
+// Per-pixel group id through the production classifier (fast_group, exact
+// fallback) and exact HSV: validation of the device arithmetic.
+__global__ void k_debug_hsv(const uint8_t* __restrict__ img, long n, GridParams gp, FastCls fc,
+                            const ClassTables* __restrict__ tabs, const double* __restrict__ k255,
+                            int* __restrict__ gid, double* __restrict__ hsv) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-        double h, s, v;
-        rgb2hsv(k255[img[3 * i]], k255[img[3 * i + 1]], k255[img[3 * i + 2]], h, s, v);
-        gid[i] = group_of(gp, h, s, v);
+        const int kr = img[3 * i], kg = img[3 * i + 1], kb = img[3 * i + 2];
+        int g = fast_group(kr, kg, kb, tabs->vcol, tabs->vgray, gp, fc);
+        if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
+        gid[i] = g;
         if (hsv) {
+            double h, s, v;
+            rgb2hsv(k255[kr], k255[kg], k255[kb], h, s, v);
             hsv[3 * i] = h;
             hsv[3 * i + 1] = s;
             hsv[3 * i + 2] = v;
@@ -412,6 +497,19 @@ __global__ void k_fill_uniform(uint8_t* __restrict__ dst, size_t n, unsigned lon
 
 }  // namespace
 
+int g_ablate = 0;   // timing experiments only (phd_debug_time_kernel)
+
+int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        hipDeviceProp_t p;
+        n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess)
+                ? p.multiProcessorCount : 256;
+    }
+    return n;
+}
+
 static inline long hsv_pixels(int height, int width, int ds, int* nw) {
     const int hh = ds > 1 ? height / ds : height, ww = ds > 1 ? width / ds : width;
     *nw = ww;
@@ -419,17 +517,19 @@ static inline long hsv_pixels(int height, int width, int ds, int* nw) {
 }
 
 hipError_t launch_hsv_stats(const uint8_t* img, int height, int width, int ds, const GridParams& gp,
-                            const PaletteDev& out, int nchunks, const double* k255, hipStream_t st) {
+                            const FastCls& fc, const ClassTables* tabs, const PaletteDev& out, int nchunks,
+                            const double* k255, hipStream_t st) {
     int nw;
     const long n = hsv_pixels(height, width, ds, &nw);
     const size_t lds = K1Lds::hist + sizeof(unsigned) * ((gp.tl + 3) & ~3);
     if (ds <= 1) {
         const int aligned = (reinterpret_cast<uintptr_t>(img) & 3) == 0;
-        hipLaunchKernelGGL(k_hsv_stats, dim3(nchunks), dim3(kThreads), lds, st, img, n, gp, k255,
-                           aligned, out);
+        const int grid = std::min(nchunks, 2 * num_cus());
+        hipLaunchKernelGGL(k_hsv_stats, dim3(grid), dim3(kK1Threads), lds, st, img, n, nchunks, gp, fc, tabs,
+                           k255, aligned, out, g_ablate);
     } else {
-        hipLaunchKernelGGL(k_hsv_ds, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp,
-                           k255, out);
+        hipLaunchKernelGGL(k_hsv_ds, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
+                           tabs, k255, out);
         const long nbytes = 3L * height * width;
         const int blocks = (int)std::min<long>(2048, (nbytes / 3 + kThreads - 1) / kThreads);
         hipLaunchKernelGGL(k_stats, dim3(blocks), dim3(kThreads), 0, st, img, nbytes, out.sums);
@@ -462,9 +562,9 @@ hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds
     return hipGetLastError();
 }
 
-hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const double* k255, int* gid,
-                            double* hsv, hipStream_t st) {
-    hipLaunchKernelGGL(k_debug_hsv, dim3(2048), dim3(256), 0, st, img, n, gp, k255, gid, hsv);
+hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
+                            const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st) {
+    hipLaunchKernelGGL(k_debug_hsv, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
     return hipGetLastError();
 }
 

@@ -191,6 +191,21 @@ void KernelProfiler::collect() {
     pending.clear();
 }
 
+const Context::Cls* get_cls(Context* c, const GridParams& gp) {
+    auto key = std::make_tuple(gp.hp, gp.sp, gp.vp, gp.bt, gp.gt);
+    auto it = c->cls.find(key);
+    if (it != c->cls.end()) return &it->second;
+    Context::Cls e;
+    ClassTables t;
+    make_class_tables(gp, &e.fc, &t);
+    if (hipMalloc(&e.d, sizeof(ClassTables)) != hipSuccess ||
+        hipMemcpy(e.d, &t, sizeof(ClassTables), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("classification table upload failed");
+        return nullptr;
+    }
+    return &(c->cls[key] = e);
+}
+
 }  // namespace phd
 
 extern "C" int phd_profile_kernels(unsigned mask) {

@@ -37,6 +37,8 @@ struct GroupCenters {
     std::vector<double> h, s, v;
 };
 GroupCenters make_centers(const GridParams& gp);
+// Exact classification tables for fast_group (phd_device.h).
+void make_class_tables(const GridParams& gp, FastCls* fc, ClassTables* t);
 
 // ---- palette decisions (host) ---------------------------------------------
 struct PaletteDecision {
@@ -91,6 +93,11 @@ struct Context {
     double* d_k255 = nullptr;                       // k/255.0 for k in [0,256)
     std::map<int, FftPlanHost> plans;
     std::map<std::tuple<int, int, int, int>, BlurTable> tables;
+    struct Cls {
+        FastCls fc;
+        ClassTables* d = nullptr;
+    };
+    std::map<std::tuple<int, int, int, double, double>, Cls> cls;
     // grow-only workspaces
     void* d_ws = nullptr;
     size_t ws_bytes = 0;
@@ -110,6 +117,8 @@ bool ensure_device(void** p, size_t* cap, size_t need);
 bool ensure_pinned(Context* c, size_t need);
 const FftPlanHost* get_plan(Context* c, int n);
 const BlurTable* get_table(Context* c, int height, int width, int nr, int na);
+// Classification tables of a grid (uploaded once per configuration).
+const Context::Cls* get_cls(Context* c, const GridParams& gp);
 
 // ---- the pipeline -----------------------------------------------------------
 struct ImageIn {

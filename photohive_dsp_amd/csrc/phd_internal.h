@@ -23,6 +23,23 @@ struct GridParams {
     double Lh, Ls, Lv, bt, gt;
 };
 
+// Exact pixel classification from integer/table facts + an fp32 estimate
+// (built on the host from the reference's double expressions, see
+// make_class_tables).  vcol/vgray live in device memory (256 entries each);
+// a pixel whose fp32 hue/saturation quotient lies within a guard band of a
+// bin boundary is sent to the exact fp64 path (phd_device.h: group_of).
+struct FastCls {
+    float gt, inv_ls, inv_lh, guard_s, guard_h;
+    int si_full, si_zero;      // Si for s == 0.999999 / s == 0 (-1 = gray)
+    int hx[9];                 // Hi for (max channel c, num == 0 / +kd / -kd)
+    int gray_base;             // TL - (ng + 1)
+};
+struct ClassTables {           // device copy, staged into LDS by the kernels
+    double rinv[256];          // 1 / k, k > 0  (saturation sums: s ~ (kmax-kmin)/kmax)
+    short vcol[256];           // Vi of v(kmax), or -1 when v < black_thresh
+    short vgray[256];          // gray group offset of v(kmax)
+};
+
 // Per-image device workspace views used by the palette kernels.
 struct PaletteDev {
     unsigned long long* sums;     // [6] sum k_r, k_g, k_b, k_r^2, k_g^2, k_b^2 (full image)
@@ -56,10 +73,12 @@ struct FftPlan {
 };
 
 // ---- launchers (kernels in *.hip) ------------------------------------------
+extern int g_ablate;   // ablation mask read by kernels under phd_debug_time_kernel
+int num_cus();         // compute units of the current device
 // hsv/stats/histogram pass over one image (K1).  ds = downsample rate.
 hipError_t launch_hsv_stats(const uint8_t* img, int height, int width, int ds,
-                            const GridParams& gp, const PaletteDev& out, int nchunks,
-                            const double* k255, hipStream_t st);
+                            const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
+                            const PaletteDev& out, int nchunks, const double* k255, hipStream_t st);
 // Locate the keep cutoff / last pixel for groups with rule.partial (Kcut).
 hipError_t launch_palette_cutoffs(const uint8_t* img, int height, int width, int ds,
                                   const GridParams& gp, const unsigned short* chunk_hist,
@@ -83,8 +102,8 @@ hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPl
                            double* fmax_part, hipStream_t st);
 // Column blocks of launch_fft_cols (= entries of fmax_part); optional LDS size.
 int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds, int* lds_bins);
-hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const double* k255, int* gid,
-                            double* hsv, hipStream_t st);
+hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
+                            const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st);
 hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st);
 // Laplacian-variance sharpness of n crop boxes: sums[2k] = sum f, sums[2k+1] =
 // sum (f - mean)^2 (sums zeroed by the caller).

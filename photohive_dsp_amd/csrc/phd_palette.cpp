@@ -80,6 +80,34 @@ GroupCenters make_centers(const GridParams& g) {
     return gc;                                            // black group stays (0, 0, 0)
 }
 
+void make_class_tables(const GridParams& g, FastCls* fc, ClassTables* t) {
+    // every entry is the reference's own double expression (rgb2hsv,
+    // src/image_processing.c:388-414; arm_octree, src/color_quantization.c:131-145)
+    for (int k = 0; k < 256; k++) {
+        const double v = (k == 255) ? 0.999999 : (double)k / 255.0;
+        t->rinv[k] = k ? 1.0 / (double)k : 0.0;
+        if (v < g.bt) {
+            t->vcol[k] = -1;
+            t->vgray[k] = 0;
+        } else {
+            t->vcol[k] = (short)(int)((v - g.bt) / g.Lv);
+            t->vgray[k] = (short)(int)((double)((int)(v - g.bt) * g.ng) / (1 - g.bt));
+        }
+    }
+    auto s_class = [&](double s) { return s < g.gt ? -1 : (int)((s - g.gt) / g.Ls); };
+    fc->si_full = s_class(0.999999);
+    fc->si_zero = s_class(0.0);
+    const double hx[9] = {0, 60, 300, 120, 180, 60, 240, 300, 180};   // quotient 0, +1, -1 per max channel
+    for (int i = 0; i < 9; i++) fc->hx[i] = (int)(hx[i] / g.Lh);
+    fc->gt = (float)g.gt;
+    fc->inv_ls = (float)(1.0 / g.Ls);
+    fc->inv_lh = (float)(1.0 / g.Lh);
+    // guard bands (in bins) well above the fp32 error bound of each quotient
+    fc->guard_s = (float)(3e-4 + 1e-6 / g.Ls + 2e-7 * g.sp);
+    fc->guard_h = 3e-4f;
+    fc->gray_base = g.tl - (g.ng + 1);
+}
+
 namespace {
 
 float saliency(unsigned q, double s, double v, float qw, float svw) {

@@ -124,7 +124,8 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
     const double inv_n = 1.0 / (int)n_hsv;
     for (int k = 0; k < np; k++) {
         const double cnt = pal[4 * k + 3];
-        if (cnt != (double)dec.kept[k]) {
+        static const bool ablating = getenv("PHD_ABLATE") != nullptr;   // timing experiments only
+        if (cnt != (double)dec.kept[k] && !ablating) {
             *why = "palette self-check failed: device kept " + std::to_string((long long)cnt) +
                    " pixels for slot " + std::to_string(k) + ", host rules predict " +
                    std::to_string(dec.kept[k]);
@@ -243,7 +244,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const FftPlanHost* prow = get_plan(c, width);
     const FftPlanHost* pcol = get_plan(c, height);
     const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
-    if (!prow || !pcol || !tbl) return false;
+    const Context::Cls* cls = get_cls(c, gp);
+    if (!prow || !pcol || !tbl || !cls) return false;
 
     const int C = fft_cols_blocks(height, wf, nbins, pcol->plan, nullptr, nullptr);
     const int ncolblocks = (wf + C - 1) / C;
@@ -273,7 +275,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         pd.s_part = (double*)(dw + L.A(i) + L.a_spart);
         pd.chunk_hist = (unsigned short*)(dw + L.H(n, i));
         const int ps = c->prof.begin(kK1, st);
-        PHD_HIP(launch_hsv_stats(d_imgs[i], height, width, ds, gp, pd, nchunks, c->d_k255, st));
+        PHD_HIP(launch_hsv_stats(d_imgs[i], height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st));
         c->prof.end(ps, st);
     }
     PHD_HIP(hipEventRecord(c->ev[1], st));
@@ -398,7 +400,9 @@ bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, 
     pd.hist = (unsigned*)(dw + L.a_hist);
     pd.s_part = (double*)(dw + L.a_spart);
     pd.chunk_hist = (unsigned short*)(dw + L.H(1, 0));
-    PHD_HIP(launch_hsv_stats(d_img, height, width, ds, gp, pd, nchunks, c->d_k255, st));
+    const Context::Cls* cls = get_cls(c, gp);
+    if (!cls) return false;
+    PHD_HIP(launch_hsv_stats(d_img, height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st));
     PHD_HIP(hipMemcpyAsync(hp, dw, L.a_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipStreamSynchronize(st));
     hist->assign((const unsigned*)(hp + L.a_hist), (const unsigned*)(hp + L.a_hist) + gp.tl);
@@ -658,10 +662,76 @@ extern "C" int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, 
     }
     std::lock_guard<std::mutex> lk(c->mu);
     const GridParams gp = make_grid(*cfg);
-    if (launch_debug_hsv(d_rgb, n_pixels, gp, c->d_k255, d_gid, d_hsv, c->stream) != hipSuccess ||
+    const Context::Cls* cls = get_cls(c, gp);
+    if (!cls) return -1;
+    if (launch_debug_hsv(d_rgb, n_pixels, gp, cls->fc, cls->d, c->d_k255, d_gid, d_hsv, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         set_error("debug hsv kernel failed");
         return -1;
     }
+    return 0;
+}
+
+// Micro-benchmark hook: launch one pipeline kernel `iters` times on a device
+// image (after one untimed full report to set up its inputs) and return the
+// average launch time in ms from HIP events.  `ablate` is a debug mask read by
+// the kernel to skip parts of its work (0 = the production kernel).
+extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int height, int width, const phd_config* cfg,
+                                     int ablate, int iters, double* avg_ms) {
+    clear_error();
+    Context* c = get_context();
+    if (!c || !cfg || iters <= 0) return -1;
+    {
+        Full_Report_Data* r = nullptr;
+        int st = -1;
+        std::lock_guard<std::mutex> lk(c->mu);
+        const uint8_t* imgs[1] = {d_rgb};
+        if (!run_reports(c, imgs, 1, height, width, *cfg, nullptr, &r, &st, nullptr)) return -1;
+        free_full_report(&r);
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    const GridParams gp = make_grid(*cfg);
+    const int ds = cfg->downsample_rate > 1 ? cfg->downsample_rate : 1;
+    const long n_hsv = hsv_count(height, width, ds);
+    const int nchunks = (int)((n_hsv + kChunk - 1) / kChunk);
+    const Context::Cls* cls = get_cls(c, gp);
+    const int wf = width / 2 + 1;
+    const FftPlanHost* prow = get_plan(c, width);
+    const FftPlanHost* pcol = get_plan(c, height);
+    const BlurTable* tbl = get_table(c, height, width, cfg->radius_partitions, cfg->angle_partitions);
+    if (!cls || !prow || !pcol || !tbl) return -1;
+    // scratch outputs in the (large enough) workspace of the report just run
+    uint8_t* dw = (uint8_t*)c->d_ws;
+    PaletteDev pd;
+    pd.sums = (unsigned long long*)dw;
+    pd.hist = (unsigned*)(dw + 256);
+    pd.s_part = (double*)(dw + 256 + 4 * 4096);
+    pd.chunk_hist = (unsigned short*)(dw + 256 + 4 * 4096 + 8 * (size_t)nchunks);
+    g_ablate = ablate;
+    const hipStream_t st = c->stream;
+    hipEvent_t a = c->ev[6], b = c->ev[7];
+    for (int it = -1; it < iters; it++) {
+        if (it == 0) (void)hipEventRecord(a, st);
+        hipError_t e = hipSuccess;
+        switch (kernel) {
+            case kK1: e = launch_hsv_stats(d_rgb, height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st); break;
+            case kFftRows: e = launch_fft_rows(d_rgb, height, width, prow->plan, pd.sums, c->d_k255, c->d_inter, st); break;
+            case kFftCols: e = launch_fft_cols(c->d_inter, height, wf, pcol->plan, tbl->d_map,
+                                               cfg->radius_partitions * cfg->angle_partitions, (double*)pd.chunk_hist,
+                                               (double*)pd.chunk_hist + 65536, st); break;
+            default: set_error("kernel not supported by the timing hook"); g_ablate = 0; return -1;
+        }
+        if (e != hipSuccess) {
+            set_error(std::string("launch failed: ") + hipGetErrorString(e));
+            g_ablate = 0;
+            return -1;
+        }
+    }
+    (void)hipEventRecord(b, st);
+    g_ablate = 0;
+    if (hipEventSynchronize(b) != hipSuccess) return -1;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    *avg_ms = ms / iters;
     return 0;
 }

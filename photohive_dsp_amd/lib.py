@@ -70,6 +70,9 @@ lib.phd_profile_kernels.argtypes = [ctypes.c_uint]
 lib.phd_profile_read.restype = ctypes.c_int
 lib.phd_profile_read.argtypes = [ctypes.c_int, P(ctypes.c_double), P(ctypes.c_long)]
 KERNELS = ["hsv_stats", "fft_rows", "fft_cols", "palette_cutoffs", "palette_sums", "sharpness"]
+lib.phd_debug_time_kernel.restype = ctypes.c_int
+lib.phd_debug_time_kernel.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(PhdConfig),
+                                      ctypes.c_int, ctypes.c_int, P(ctypes.c_double)]
 lib.free_full_report.restype = None
 lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
 lib.phd_free_pgm.argtypes = [P(Image_PGM)]
