@@ -143,6 +143,16 @@ int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int height, int 
                             size_t image_stride, const phd_config* cfg, Full_Report_Data** out,
                             int* status, void* stream);
 
+/* rgb2hsv + get_hsv_average + get_rgb_statistics over n device-resident RGB8
+ * images (BASELINE.json config 3).  Replaces the reference's
+ * rgb2hsv (src/image_processing.c:372-417), get_hsv_average (:533-540) and
+ * get_rgb_statistics (:543-553) as called from get_full_report_data
+ * (src/interface.c:46-55) with downsample_rate 1; the HSV image itself is never
+ * materialised.  stats[i] / avg_saturation[i] per image.  0 or -1. */
+int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
+                               size_t image_stride, RGB_Statistics* stats, double* avg_saturation,
+                               void* stream);
+
 /* A batch of host images of any sizes (config 5 of BASELINE.json). */
 int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
                         int n_images, const phd_config* cfg, Full_Report_Data** out, int* status);

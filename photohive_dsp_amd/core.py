@@ -18,7 +18,7 @@ from types import SimpleNamespace
 import numpy as np
 
 from .lib import last_error, lib
-from .structures import Crop_Boundaries, Full_Report_Data, PhdConfig, Pixel_HSV
+from .structures import Crop_Boundaries, Full_Report_Data, PhdConfig, Pixel_HSV, RGB_Statistics
 from .utils import hsv_to_rgb, image_pgm_to_pillow, to_rgb8
 
 DEFAULTS = dict(h_partitions=18, s_partitions=2, v_partitions=3, black_thresh=0.1, gray_thresh=0.1,
@@ -213,6 +213,21 @@ def report_device(images, stream=None, **kw):
     if any(r is None for r in res):
         raise RuntimeError(f"report_device failed: {last_error()}")
     return res
+
+
+def hsv_stats_device(images, stream=None):
+    """rgb2hsv + get_hsv_average + get_rgb_statistics (src/image_processing.c:372-417, 533-553)
+    for a uint8 torch tensor [N, H, W, 3] on the current GPU: returns
+    ([RGB_Statistics] * N, [average saturation] * N)."""
+    if images.dtype.itemsize != 1 or images.dim() != 4 or images.shape[3] != 3 or not images.is_contiguous():
+        raise ValueError("expected a contiguous uint8 [N, H, W, 3] device tensor")
+    n, h, w = int(images.shape[0]), int(images.shape[1]), int(images.shape[2])
+    stats = (RGB_Statistics * n)()
+    sat = (ctypes.c_double * n)()
+    s = stream.cuda_stream if stream is not None else None
+    if lib.phd_hsv_stats_batch_device(images.data_ptr(), n, h, w, 0, stats, sat, s) != 0:
+        raise RuntimeError(f"hsv_stats_device failed: {last_error()}")
+    return list(stats), list(sat)
 
 
 def set_bounding_boxes(bounding_boxes):

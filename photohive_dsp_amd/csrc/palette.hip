@@ -24,23 +24,27 @@ constexpr int kQueue = kChunk;               // deferred exact-path pixels (u16 
 constexpr int kK1Threads = 1024;             // K1 block: 16 waves over one kChunk
 struct K1Lds {
     static constexpr int k255 = 0;           // 256 doubles
-    static constexpr int rinv = 2048;        // 256 doubles
-    static constexpr int vcol = 4096;        // 256 int16
-    static constexpr int vgray = 4608;       // 256 int16
-    static constexpr int red = 5120;         // 16 waves x 8 x u64
-    static constexpr int qn = 6144;          // int (+pad)
-    static constexpr int queue = 6160;       // kQueue x u16 (pixel offset in the chunk)
-    static constexpr int hist = 6160 + 2 * kQueue;   // tl x u32
+    static constexpr int ent = 2048;         // 256 ClsEnt (16 B)
+    static constexpr int red = 6144;         // 16 waves x 8 x u64
+    static constexpr int qn = 7168;          // 2 ints (+pad)
+    static constexpr int si8 = 7184;         // 256 x 256 int8 saturation classes
+    static constexpr int queue = si8 + 65536;   // kQueue x u16 (pixel offset in the chunk)
+    static constexpr int hist = queue + 2 * kQueue;   // tl x u32 (K1: 3 x tl)
 };
+static_assert(sizeof(ClsEnt) == 16, "ClsEnt is one 16-B LDS read");
 
 __device__ __forceinline__ void stage_tables(unsigned char* smem, const double* __restrict__ k255g,
-                                             const ClassTables* __restrict__ tabs) {
+                                             const ClassTables* __restrict__ tabs, bool with_si8 = true) {
     const int tid = threadIdx.x;
-    if (tid >= 256) return;
-    reinterpret_cast<double*>(smem + K1Lds::k255)[tid] = k255g[tid];
-    reinterpret_cast<double*>(smem + K1Lds::rinv)[tid] = tabs->rinv[tid];
-    reinterpret_cast<short*>(smem + K1Lds::vcol)[tid] = tabs->vcol[tid];
-    reinterpret_cast<short*>(smem + K1Lds::vgray)[tid] = tabs->vgray[tid];
+    if (tid < 256) {
+        reinterpret_cast<double*>(smem + K1Lds::k255)[tid] = k255g[tid];
+        reinterpret_cast<ClsEnt*>(smem + K1Lds::ent)[tid] = tabs->ent[tid];
+    }
+    if (with_si8) {
+        const uint4* src = reinterpret_cast<const uint4*>(tabs->si8);
+        uint4* dst = reinterpret_cast<uint4*>(smem + K1Lds::si8);
+        for (int i = tid; i < 65536 / 16; i += blockDim.x) dst[i] = src[i];
+    }
 }
 
 __device__ __forceinline__ void load4(const uint8_t* __restrict__ img, long p0, long end,
@@ -71,26 +75,7 @@ __device__ __forceinline__ void load4(const uint8_t* __restrict__ img, long p0, 
     }
 }
 
-// Raw form of load4: the three little-endian words holding pixels p0..p0+3
-// (bytes past `end` are zero); unpack with px_byte.
-__device__ __forceinline__ int load4_raw(const uint8_t* __restrict__ img, long p0, long end, bool aligned,
-                                         unsigned (&w)[3]) {
-    if (aligned && p0 + 3 < end) {
-        const unsigned* q = reinterpret_cast<const unsigned*>(img + 3 * p0);
-        w[0] = q[0];
-        w[1] = q[1];
-        w[2] = q[2];
-        return 4;
-    }
-    w[0] = w[1] = w[2] = 0;
-    int nv = 0;
-    for (int b = 0; b < 12; b++)
-        if (p0 + b / 3 < end) {
-            w[b >> 2] |= (unsigned)img[3 * p0 + b] << (8 * (b & 3));
-            nv = b / 3 + 1;
-        }
-    return nv;
-}
+typedef const __attribute__((address_space(1))) unsigned gu32;   // global (not flat) loads
 
 __device__ __forceinline__ int px_byte(const unsigned (&w)[3], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255; }
 
@@ -106,105 +91,269 @@ __device__ __forceinline__ void hist_add(unsigned* lds, int g) {
     }
 }
 
-// K1 for downsample_rate == 1: stats and HSV over the same pixels.
-// Persistent blocks (2 per CU) walk the image's kChunk-pixel chunks; per chunk
-// the group histogram is built in LDS and written out (the cutoff search walks
-// these per-chunk counts); channel moments and sum(s) stay in registers and are
-// reduced once per block.  Pixels classify through fast_group; the few near a
-// bin edge are queued in LDS and classified exactly after the chunk's stream,
-// so waves stay convergent.  Next-chunk loads are issued before the current
-// chunk's flush.
-__global__ __launch_bounds__(kK1Threads, 8) void k_hsv_stats(const uint8_t* __restrict__ img, long npix,
-                                                        int nchunks, GridParams gp, FastCls fc,
-                                                        const ClassTables* __restrict__ tabs,
-                                                        const double* __restrict__ k255g,
-                                                        int aligned, PaletteDev out, int ablate) {
+#ifndef PHD_K1_ABLATE
+#define PHD_K1_ABLATE 0        // K1 ablation mask for timing builds (16 hist, 32 sat, 128 atomics)
+#endif
+#ifndef PHD_K1_MINWAVES
+#define PHD_K1_MINWAVES 8        // waves/SIMD the statistics-only K1 is sized for (2 blocks/CU)
+#endif
+#ifndef PHD_K1_MINWAVES_HIST
+#define PHD_K1_MINWAVES_HIST 4   // histogram K1: its 64 KiB table allows 1 block/CU anyway
+#endif
+
+// Per-image outputs of a batch: image i's records sit at i * stride bytes.
+__device__ __forceinline__ unsigned long long* img_sums(const PaletteDev& o, long a_stride, int i) {
+    return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(o.sums) + i * a_stride);
+}
+__device__ __forceinline__ unsigned* img_hist(const PaletteDev& o, long a_stride, int i) {
+    return reinterpret_cast<unsigned*>(reinterpret_cast<char*>(o.hist) + i * a_stride);
+}
+__device__ __forceinline__ double* img_spart(const PaletteDev& o, long a_stride, int i) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(o.s_part) + i * a_stride);
+}
+__device__ __forceinline__ unsigned short* img_chunks(const PaletteDev& o, long h_stride, int i) {
+    return reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(o.chunk_hist) + i * h_stride);
+}
+
+typedef const __attribute__((address_space(1))) uint8_t gu8;
+
+// The 12 bytes of pixels p0..p0+3 of an image as three little-endian words.
+// Groups not wholly inside the image load from pixel 0 and are masked by the
+// caller (the `ok` bits); so every load is unconditional and stays in flight.
+template <bool kAligned>
+__device__ __forceinline__ void load_group(const uint8_t* ip, long p0, bool ok, unsigned (&w)[3]) {
+    const long a = ok ? 3 * p0 : 0;
+    if (kAligned) {
+        gu32* q = (gu32*)(ip + a);
+        w[0] = q[0];
+        w[1] = q[1];
+        w[2] = q[2];
+    } else {
+        gu8* b = (gu8*)(ip + a);
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            w[k] = (unsigned)b[4 * k] | (unsigned)b[4 * k + 1] << 8 | (unsigned)b[4 * k + 2] << 16 |
+                   (unsigned)b[4 * k + 3] << 24;
+    }
+}
+
+// hist_add for a fully active wave whose g are all valid slots (K1's deferred
+// pixels count into a dummy slot): one atomic per wave when the whole wave
+// hits one group (flat regions), else one per lane.
+__device__ __forceinline__ void hist_add_full(unsigned* lds, int g) {
+    const int g0 = __builtin_amdgcn_readfirstlane(g);
+    if (__builtin_amdgcn_ballot_w64(g != g0) == 0) {
+        if (lane_id() == 0) atomicAdd(&lds[g0], 64u);
+    } else {
+        atomicAdd(&lds[g], 1u);
+    }
+}
+
+// K1 for downsample_rate == 1, over a whole batch of same-size images in one
+// launch: channel moments, sum(s) and (kHist) the group histogram.
+//
+// The batch is a sequence of (image, chunk) work items of kChunk pixels; each
+// persistent block (2 per CU) takes one contiguous run of items, so it crosses
+// at most a few image boundaries.  Moments and sum(s) stay in registers and
+// are flushed (block reduction + one atomic per counter) when the run leaves
+// an image.  The per-chunk group counts are built in LDS (double-buffered, so
+// a chunk costs two barriers), written out for the cutoff search, and summed
+// into a per-run LDS histogram that is flushed with the moments.  Pixels
+// classify through classify(); the few near a bin edge are queued and
+// classified exactly after the chunk's stream so waves stay convergent.  The
+// next item's loads are issued before the current chunk's barriers.
+// kHist == false is the rgb2hsv + statistics pass alone (S-bar and moments).
+//
+// Each thread owns kSteps groups of 4 pixels (12 bytes, one dwordx3) per
+// chunk, a wave reading 768 contiguous bytes per group step.  Groups past the
+// image end are masked to (0, 0, 0) pixels, which add nothing to the moments
+// or sum(s) and are taken back out of the histogram; the < 4 pixels of a
+// partial final group are done by one thread of the last chunk.
+template <bool kHist, bool kAligned>
+__global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_MINWAVES) void k_hsv_stats(
+        const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
+        const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, PaletteDev out, long a_stride,
+        long h_stride) {
+    constexpr int ablate = PHD_K1_ABLATE;   // compile-time ablation (timing builds only)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
-    const double* rinv = reinterpret_cast<const double*>(smem + K1Lds::rinv);
-    const short* vcol = reinterpret_cast<const short*>(smem + K1Lds::vcol);
-    const short* vgray = reinterpret_cast<const short*>(smem + K1Lds::vgray);
+    const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
+    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + K1Lds::red);
     int* qn = reinterpret_cast<int*>(smem + K1Lds::qn);
     unsigned short* queue = reinterpret_cast<unsigned short*>(smem + K1Lds::queue);
-    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);
+    const int tl = gp.tl;
+    const int tl1 = tl + 1;                                             // + dummy slot (deferred pixels)
+    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);   // [2][tl1] chunk counts
+    unsigned* seg = lh + 2 * tl1;                                      // [tl] counts of the run
     const int tid = threadIdx.x;
-    stage_tables(smem, k255g, tabs);
-    unsigned long long mom[6] = {0, 0, 0, 0, 0, 0};
-    double ssum = 0.0;
-    constexpr int kSteps = kChunk / (4 * kK1Threads);
-    unsigned w[kSteps][3];
-    int nv[kSteps];
-    auto issue = [&](int c) {
-        const long base = (long)c * kChunk, end = min(base + (long)kChunk, npix);
-#pragma unroll
-        for (int it = 0; it < kSteps; it++)
-            nv[it] = load4_raw(img, base + 4L * tid + 4L * kK1Threads * it, end, aligned != 0, w[it]);
-    };
-    int c = blockIdx.x;
-    if (c < nchunks) issue(c);
-    for (; c < nchunks; c += gridDim.x) {
-        for (int i = tid; i < gp.tl; i += kK1Threads) lh[i] = 0;
-        if (tid == 0) *qn = 0;
-        __syncthreads();
-        const long base = (long)c * kChunk;
-        unsigned sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
-#pragma unroll
-        for (int it = 0; it < kSteps; it++) {
-            const long p0 = base + 4L * tid + 4L * kK1Threads * it;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int kr = px_byte(w[it], 3 * i), kg = px_byte(w[it], 3 * i + 1), kb = px_byte(w[it], 3 * i + 2);
-                const bool valid = i < nv[it];
-                if (valid) {
-                    sr += kr; sg += kg; sb += kb;
-                    qr += kr * kr; qg += kg * kg; qb += kb * kb;
-                }
-                if (!(ablate & 32)) ssum += valid ? sat_of(kr, kg, kb, rinv) : 0.0;
-                int g = !valid ? -1 : (ablate & 8) ? (kr & 7) : fast_group(kr, kg, kb, vcol, vgray, gp, fc);
-                if (g == -2) {                // near a bin edge: classify exactly after the stream
-                    queue[atomicAdd(qn, 1)] = (unsigned short)(p0 + i - base);
-                    g = -1;
-                }
-                if (!(ablate & 16)) hist_add(lh, g);
-                else if (g >= 0) ssum += g;
-            }
-        }
-        mom[0] += sr; mom[1] += sg; mom[2] += sb; mom[3] += qr; mom[4] += qg; mom[5] += qb;
-        if (c + (int)gridDim.x < nchunks) issue(c + gridDim.x);   // prefetch the next chunk
-        __syncthreads();
-        const int nq = *qn;
-        for (int q = tid; q < nq; q += kK1Threads) {
-            const long p = base + queue[q];
-            atomicAdd(&lh[exact_group(img[3 * p], img[3 * p + 1], img[3 * p + 2], k255, gp)], 1u);
-        }
-        __syncthreads();
-        for (int i = tid; i < gp.tl; i += kK1Threads) {
-            const unsigned n = lh[i];
-            out.chunk_hist[(long)c * gp.tl + i] = (unsigned short)n;
-            if (n && !(ablate & 128)) atomicAdd(&out.hist[i], n);
-        }
-        __syncthreads();
-    }
-    // block reduction of the integer moments (exact) and of sum(s), once
-    const int wv = tid >> 6;
-#pragma unroll
-    for (int k = 0; k < 6; k++) mom[k] = wave_sum(mom[k]);
-    const double sw = wave_sum(ssum);
-    if (lane_id() == 0) {
-#pragma unroll
-        for (int k = 0; k < 6; k++) red[wv * 8 + k] = mom[k];
-        reinterpret_cast<double*>(red)[wv * 8 + 6] = sw;
+    const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
+    if (it0 >= it1) return;                                 // block-uniform
+    stage_tables(smem, k255g, tabs, kHist);
+    if (kHist) {
+        for (int i = tid; i < 2 * tl1 + tl; i += kK1Threads) lh[i] = 0;
+        if (tid < 2) qn[tid] = 0;
     }
     __syncthreads();
-    if (tid < 6) {
-        unsigned long long t = 0;
-        for (int q = 0; q < kK1Threads / 64; q++) t += red[q * 8 + tid];
-        if (!(ablate & 128)) atomicAdd(&out.sums[tid], t);
-    } else if (tid == 6) {
-        double t = 0.0;
-        for (int q = 0; q < kK1Threads / 64; q++) t += reinterpret_cast<double*>(red)[q * 8 + 6];
-        out.s_part[blockIdx.x] = t;        // one partial per block (host sums them)
+
+    constexpr int kSteps = kChunk / (4 * kK1Threads);
+    static_assert(kSteps >= 2 && kSteps <= 8, "K1 step count");
+    const long full_end = npix & ~3L;                       // groups wholly inside the image
+    unsigned w[kSteps][3];
+    unsigned okb = 0;                                       // bit st: group st is inside
+    auto issue = [&](const uint8_t* ip, int c) {
+        okb = 0;
+#pragma unroll
+        for (int st = 0; st < kSteps; st++) {
+            const long p0 = (long)c * kChunk + 4L * tid + 4L * kK1Threads * st;
+            const bool ok = p0 < full_end;
+            okb |= (unsigned)ok << st;
+            load_group<kAligned>(ip, p0, ok, w[st]);
+        }
+    };
+    int img = (int)(it0 / nchunks), c = (int)(it0 - (long)img * nchunks);
+    const uint8_t* ip = imgs[img];
+    issue(ip, c);
+    // per-thread moments of the current run: u32 holds 4096 chunks of squares
+    // (16 px * 255^2 each), so a run is flushed at the latest after 4096 chunks
+    unsigned sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
+    double ssum = 0.0;
+    int seg_c0 = c, par = 0;
+    long seg_it0 = it0;
+    for (long it = it0; it < it1; it++, par ^= 1) {
+        unsigned* ch = lh + par * tl1;
+        const long base = (long)c * kChunk;
+        // one group (4 pixels) per iteration; the words rotate through
+        // registers so the loop is not unrolled (bounded live state)
+        unsigned bits = okb;
+        unsigned c0 = (bits & 1) ? w[0][0] : 0u, c1 = (bits & 1) ? w[0][1] : 0u, c2 = (bits & 1) ? w[0][2] : 0u;
+#pragma unroll 1
+        for (int st = 0; st < kSteps; st++) {
+            const int o0 = 4 * tid + 4 * kK1Threads * st;     // offset in the chunk
+            const unsigned cw[3] = {c0, c1, c2};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int kr = px_byte(cw, 3 * i), kg = px_byte(cw, 3 * i + 1), kb = px_byte(cw, 3 * i + 2);
+                sr += kr; sg += kg; sb += kb;
+                qr += kr * kr; qg += kg * kg; qb += kb * kb;
+                if (kHist) {
+                    double sv;
+                    int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+                    if (!(ablate & 32)) ssum += sv;
+                    if (g == -2) {            // on a hue bin edge: classify exactly after the stream
+                        queue[atomicAdd(&qn[par], 1)] = (unsigned short)(o0 + i);
+                        g = tl;
+                    }
+                    if (!(ablate & 16)) hist_add_full(ch, g);
+                } else {
+                    if (!(ablate & 32)) ssum += sat_only(kr, kg, kb, ent);
+                }
+            }
+            bits >>= 1;
+            const bool okn = bits & 1;
+            c0 = okn ? w[1][0] : 0u;
+            c1 = okn ? w[1][1] : 0u;
+            c2 = okn ? w[1][2] : 0u;
+#pragma unroll
+            for (int k = 1; k + 1 < kSteps; k++) {
+                w[k][0] = w[k + 1][0]; w[k][1] = w[k + 1][1]; w[k][2] = w[k + 1][2];
+            }
+        }
+        const bool last_chunk = base + kChunk >= npix;         // block-uniform
+        const int tail = (int)(npix & 3);
+        if (last_chunk && tail && tid == 0) {
+            // the partial final group of the image: one lane, plain atomics
+            for (long p = full_end; p < npix; p++) {
+                const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
+                sr += kr; sg += kg; sb += kb;
+                qr += kr * kr; qg += kg * kg; qb += kb * kb;
+                double sv;
+                if (kHist) {
+                    int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+                    if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
+                    atomicAdd(&ch[g], 1u);
+                } else {
+                    sv = sat_only(kr, kg, kb, ent);
+                }
+                ssum += sv;
+            }
+        }
+        // next work item: prefetch its pixels now
+        const int cimg = img, cc = c;
+        const uint8_t* cip = ip;
+        if (++c == nchunks) {
+            c = 0;
+            img++;
+        }
+        const bool more = it + 1 < it1;
+        if (more) {
+            if (img != cimg) ip = imgs[img];
+            issue(ip, c);
+        }
+        if (kHist) {
+            __syncthreads();
+            // zero pixels of masked groups (a whole-group count per chunk)
+            const long pad = base + kChunk - full_end;
+            if (pad > 0 && tid == 0) {
+                double sv;
+                atomicSub(&ch[classify(0, 0, 0, ent, si8, gp, fc, sv)], (unsigned)pad);
+            }
+            const int nq = qn[par];
+            for (int q = tid; q < nq; q += kK1Threads) {
+                const long p = base + queue[q];
+                atomicAdd(&ch[exact_group(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp)], 1u);
+            }
+            __syncthreads();
+            unsigned short* chunk_out = img_chunks(out, h_stride, cimg) + (long)cc * tl;
+            for (int i = tid; i < tl; i += kK1Threads) {
+                const unsigned n = ch[i];
+                chunk_out[i] = (unsigned short)n;
+                seg[i] += n;
+                ch[i] = 0;
+            }
+            if (tid == 0) {
+                qn[par] = 0;
+                ch[tl] = 0;
+            }
+        }
+        if (!more || img != cimg || it + 1 - seg_it0 == 4096) {
+            // the run leaves image cimg (or its u32 moments could overflow):
+            // flush its moments, sum(s) and counts
+            const int wv = tid >> 6;
+            const unsigned mom[6] = {sr, sg, sb, qr, qg, qb};
+            unsigned long long m64[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) m64[k] = wave_sum((unsigned long long)mom[k]);
+            const double sw = wave_sum(ssum);
+            if (lane_id() == 0) {
+#pragma unroll
+                for (int k = 0; k < 6; k++) red[wv * 8 + k] = m64[k];
+                reinterpret_cast<double*>(red)[wv * 8 + 6] = sw;
+            }
+            __syncthreads();
+            if (tid < 6) {
+                unsigned long long t = 0;
+                for (int q = 0; q < kK1Threads / 64; q++) t += red[q * 8 + tid];
+                if (!(ablate & 128)) atomicAdd(&img_sums(out, a_stride, cimg)[tid], t);
+            } else if (tid == 6) {
+                double t = 0.0;
+                for (int q = 0; q < kK1Threads / 64; q++) t += reinterpret_cast<double*>(red)[q * 8 + 6];
+                img_spart(out, a_stride, cimg)[seg_c0] = t;   // one slot per run (host sums them)
+            }
+            if (kHist) {
+                unsigned* hist = img_hist(out, a_stride, cimg);
+                for (int i = tid; i < tl; i += kK1Threads) {
+                    const unsigned n = seg[i];
+                    if (n && !(ablate & 128)) atomicAdd(&hist[i], n);
+                    seg[i] = 0;
+                }
+            }
+            sr = sg = sb = qr = qg = qb = 0;
+            ssum = 0.0;
+            seg_c0 = c;
+            seg_it0 = it + 1;
+            __syncthreads();                                  // red is reused by the next flush
+        }
     }
 }
 
@@ -215,9 +364,8 @@ __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__
                                                      const double* __restrict__ k255g, PaletteDev out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
-    const double* rinv = reinterpret_cast<const double*>(smem + K1Lds::rinv);
-    const short* vcol = reinterpret_cast<const short*>(smem + K1Lds::vcol);
-    const short* vgray = reinterpret_cast<const short*>(smem + K1Lds::vgray);
+    const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
+    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
     double* red = reinterpret_cast<double*>(smem + K1Lds::red);
     unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);
     const int tid = threadIdx.x;
@@ -230,8 +378,9 @@ __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__
     for (long j = base + tid; j < end; j += kThreads) {
         const long p = src_pixel(j, width, ds, nw);
         const int kr = img[3 * p], kg = img[3 * p + 1], kb = img[3 * p + 2];
-        ssum += sat_of(kr, kg, kb, rinv);
-        int g = fast_group(kr, kg, kb, vcol, vgray, gp, fc);
+        double sv;
+        int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+        ssum += sv;
         if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
         hist_add(lh, g);
     }
@@ -459,14 +608,15 @@ __global__ __launch_bounds__(kThreads) void k_palette_sums(const uint8_t* __rest
     }
 }
 
-// Per-pixel group id through the production classifier (fast_group, exact
+// Per-pixel group id through the production classifier (classify, exact
 // fallback) and exact HSV: validation of the device arithmetic.
 __global__ void k_debug_hsv(const uint8_t* __restrict__ img, long n, GridParams gp, FastCls fc,
                             const ClassTables* __restrict__ tabs, const double* __restrict__ k255,
                             int* __restrict__ gid, double* __restrict__ hsv) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const int kr = img[3 * i], kg = img[3 * i + 1], kb = img[3 * i + 2];
-        int g = fast_group(kr, kg, kb, tabs->vcol, tabs->vgray, gp, fc);
+        double sv;
+        int g = classify(kr, kg, kb, tabs->ent, tabs->si8, gp, fc, sv);
         if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
         gid[i] = g;
         if (hsv) {
@@ -516,24 +666,57 @@ static inline long hsv_pixels(int height, int width, int ds, int* nw) {
     return (long)(short)hh * (short)ww;   // rgb2hsv's short dimensions, image_processing.c:378-383
 }
 
-hipError_t launch_hsv_stats(const uint8_t* img, int height, int width, int ds, const GridParams& gp,
-                            const FastCls& fc, const ClassTables* tabs, const PaletteDev& out, int nchunks,
-                            const double* k255, hipStream_t st) {
+size_t hsv_stats_lds(const GridParams& gp, bool hist) {
+    return hist ? K1Lds::hist + sizeof(unsigned) * (3 * (size_t)gp.tl + 2) : (size_t)K1Lds::si8;
+}
+
+hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width,
+                                  const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
+                                  const PaletteDev& out0, long a_stride, long h_stride, int nchunks,
+                                  const double* k255, bool hist, bool aligned, hipStream_t st) {
+    const long npix = (long)height * width;
+    const long nitems = (long)n * nchunks;
+    const size_t lds = hsv_stats_lds(gp, hist);
+    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
+    const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
+#define PHD_K1_LAUNCH(H, A)                                                                                   \
+    do {                                                                                                      \
+        static bool attr = false;                                                                             \
+        if (!attr) {                                                                                          \
+            (void)hipFuncSetAttribute((const void*)k_hsv_stats<H, A>,                                         \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                \
+            attr = true;                                                                                      \
+        }                                                                                                     \
+        hipLaunchKernelGGL((k_hsv_stats<H, A>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix, nchunks, \
+                           nitems, gp, fc, tabs, k255, out0, a_stride, h_stride);                             \
+    } while (0)
+    if (hist) {
+        if (aligned) PHD_K1_LAUNCH(true, true);
+        else PHD_K1_LAUNCH(true, false);
+    } else {
+        if (aligned) PHD_K1_LAUNCH(false, true);
+        else PHD_K1_LAUNCH(false, false);
+    }
+#undef PHD_K1_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_hsv_ds(const uint8_t* img, int height, int width, int ds, const GridParams& gp,
+                         const FastCls& fc, const ClassTables* tabs, const PaletteDev& out, int nchunks,
+                         const double* k255, hipStream_t st) {
     int nw;
     const long n = hsv_pixels(height, width, ds, &nw);
     const size_t lds = K1Lds::hist + sizeof(unsigned) * ((gp.tl + 3) & ~3);
-    if (ds <= 1) {
-        const int aligned = (reinterpret_cast<uintptr_t>(img) & 3) == 0;
-        const int grid = std::min(nchunks, 2 * num_cus());
-        hipLaunchKernelGGL(k_hsv_stats, dim3(grid), dim3(kK1Threads), lds, st, img, n, nchunks, gp, fc, tabs,
-                           k255, aligned, out, g_ablate);
-    } else {
-        hipLaunchKernelGGL(k_hsv_ds, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
-                           tabs, k255, out);
-        const long nbytes = 3L * height * width;
-        const int blocks = (int)std::min<long>(2048, (nbytes / 3 + kThreads - 1) / kThreads);
-        hipLaunchKernelGGL(k_stats, dim3(blocks), dim3(kThreads), 0, st, img, nbytes, out.sums);
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_hsv_ds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
     }
+    hipLaunchKernelGGL(k_hsv_ds, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc, tabs,
+                       k255, out);
+    const long nbytes = 3L * height * width;
+    const int blocks = (int)std::min<long>(2048, (nbytes / 3 + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(k_stats, dim3(blocks), dim3(kThreads), 0, st, img, nbytes, out.sums);
     return hipGetLastError();
 }
 

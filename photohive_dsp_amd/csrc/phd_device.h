@@ -54,41 +54,45 @@ __device__ __forceinline__ int group_of(const GridParams& gp, double h, double s
 // Lh | 360 sits >= 1/(6 kd) >= 6.5e-4 from an integer.  Exact special cases:
 // v-classes come from a table over kmax; s == 0 (kd == 0) and s == 0.999999
 // (kmin == 0); hue quotients 0 and +-1 (num == 0, +-kd) are exact in fp64.
-__device__ __forceinline__ int fast_group(int kr, int kg, int kb, const short* vcol,
-                                          const short* vgray, const GridParams& gp, const FastCls& F) {
+// Group id of a pixel (or -2: take the exact path) and its HSV saturation.
+// Vi, the gray group and Si come from tables of the reference's own double
+// results; the hue bin is exact integer arithmetic: with N = 60*num + base*d
+// and D = Lh*d (num = the channel difference of rgb2hsv's branch, d = max -
+// min, base = 0/120/240, or 360 for a negative red-sector hue), Hi = floor(N/D).
+// N, D < 2^17, so (N + 0.5) * rcp(D) in fp32 is within 0.02 of the half-way
+// gap to any integer and truncates to floor(N/D) exactly.  When D divides N
+// and num is not 0 or +-d, the reference's double hue may round either side
+// of the edge: those pixels (-2) take the fp64 path.  Select-only code.
+__device__ __forceinline__ int classify(int kr, int kg, int kb, const ClsEnt* ent, const signed char* si8,
+                                        const GridParams& gp, const FastCls& F, double& s_out) {
     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
-    const int vi = vcol[kmx];
-    if (vi < 0) return gp.tl - 1;                       // v < black_thresh
-    int si;
-    if (kd == 0) si = F.si_zero;                        // s == 0 (also kmax == 0)
-    else if (kmn == 0) si = F.si_full;                  // d == max: s = 0.999999
-    else {
-        const float sf = (float)kd * __builtin_amdgcn_rcpf((float)kmx);
-        const float q = (sf - F.gt) * F.inv_ls;
-        if (fabsf(q - rintf(q)) < F.guard_s) return -2;
-        si = q < 0.f ? -1 : (int)q;
-    }
-    if (si < 0) return F.gray_base + vgray[kmx];        // s < gray_thresh
-    int hi;
-    if (kd == 0) {
-        hi = 0;                                         // h = 0
-    } else {
-        int num, c;
-        if (kr == kmx) { num = kg - kb; c = 0; }
-        else if (kg == kmx) { num = kb - kr; c = 1; }
-        else { num = kr - kg; c = 2; }
-        if (num == 0) hi = F.hx[3 * c];
-        else if (num == kd) hi = F.hx[3 * c + 1];
-        else if (num == -kd) hi = F.hx[3 * c + 2];
-        else {
-            float h = (float)(120 * c) + (60.f * (float)num) * __builtin_amdgcn_rcpf((float)kd);
-            if (h < 0.f) h += 360.f;
-            const float q = h * F.inv_lh;
-            if (fabsf(q - rintf(q)) < F.guard_h) return -2;
-            hi = (int)q;
-        }
-    }
-    return (hi * gp.sp + si) * gp.vp + vi;
+    const ClsEnt e = ent[kmx];
+    // s exactly as rgb2hsv up to the last ulp: 0 (d == 0), 0.999999 (d == max), else d / max
+    const double s = (double)kd * e.rinv;
+    s_out = (kmn == 0 && kd != 0) ? 0.999999 : s;
+    const int si = si8[(kmx << 8) | kd];
+    // hue bin
+    const bool isr = kr == kmx, isg = kg == kmx;
+    const int a = isr ? kg : (isg ? kb : kr), b = isr ? kb : (isg ? kr : kg);
+    const int num = a - b;
+    const int base = isr ? (num < 0 ? 360 : 0) : (isg ? 120 : 240);
+    const int kd1 = max(kd, 1);
+    const int N = __mul24(base, kd1) + 60 * num, D = __mul24(F.lh, kd1);
+    const int hi = (int)(((float)N + 0.5f) * __builtin_amdgcn_rcpf((float)D));
+    const bool special = num == 0 || num == kd || num == -kd;
+    const bool edge = !special && __mul24(hi, D) == N;
+    const int vi = (e.vpack << 16) >> 16, gray = e.vpack >> 16;
+    int g = __mul24(__mul24(hi, gp.sp) + si, gp.vp) + vi;
+    g = edge ? -2 : g;
+    g = si < 0 ? gray : g;
+    return vi < 0 ? gp.tl - 1 : g;
+}
+
+// HSV saturation alone (rgb2hsv's s), for the statistics-only pass.
+__device__ __forceinline__ double sat_only(int kr, int kg, int kb, const ClsEnt* ent) {
+    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
+    double s = (double)kd * ent[kmx].rinv;   // d == 0 gives 0 (rinv[0] == 0 covers max == 0)
+    return kmn == 0 && kd != 0 ? 0.999999 : s;
 }
 
 // The reference's exact group of a pixel (rgb2hsv in fp64 + arm_octree).
@@ -96,16 +100,6 @@ __device__ __forceinline__ int exact_group(int kr, int kg, int kb, const double*
     double h, s, v;
     rgb2hsv(k255[kr], k255[kg], k255[kb], h, s, v);
     return group_of(gp, h, s, v);
-}
-
-// Saturation for the S-bar sum: kd * (1/kmax) from a table, within a few ulp
-// of the reference's (max - min) / max (get_hsv_average's contract is 1e-4
-// relative; the sum over an image agrees to ~1e-15).
-__device__ __forceinline__ double sat_of(int kr, int kg, int kb, const double* rinv) {
-    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
-    if (kmx == kmn) return 0.0;
-    if (kmn == 0) return 0.999999;
-    return (double)(kmx - kmn) * rinv[kmx];
 }
 
 // Source pixel of hsv-index j (downsample_rgb's row quirk for ds > 1:

@@ -106,6 +106,8 @@ struct Context {
     double2* d_inter = nullptr;
     size_t inter_bytes = 0;
     uint8_t* d_stage = nullptr;                    // upload staging for host images
+    void* d_ptrs = nullptr;                        // small device pointer arrays (debug hooks)
+    size_t ptrs_bytes = 0;
     size_t stage_bytes = 0;
     hipEvent_t ev[8] = {};
     KernelProfiler prof;

@@ -23,21 +23,22 @@ struct GridParams {
     double Lh, Ls, Lv, bt, gt;
 };
 
-// Exact pixel classification from integer/table facts + an fp32 estimate
-// (built on the host from the reference's double expressions, see
-// make_class_tables).  vcol/vgray live in device memory (256 entries each);
-// a pixel whose fp32 hue/saturation quotient lies within a guard band of a
-// bin boundary is sent to the exact fp64 path (phd_device.h: group_of).
+// Exact pixel classification (phd_device.h: classify) from tables built on the
+// host with the reference's own double expressions (make_class_tables) plus an
+// exact integer form of the hue bin.  Only pixels whose hue lies exactly on a
+// bin edge (where the reference's double rounding decides) take the fp64 path.
 struct FastCls {
-    float gt, inv_ls, inv_lh, guard_s, guard_h;
-    int si_full, si_zero;      // Si for s == 0.999999 / s == 0 (-1 = gray)
-    int hx[9];                 // Hi for (max channel c, num == 0 / +kd / -kd)
-    int gray_base;             // TL - (ng + 1)
+    int lh;                    // Lh = 360 / h_partitions (integer division, :41)
+};
+struct ClsEnt {                // per max channel value k (16 B: one LDS read)
+    double rinv;               // 1 / k (k > 0; 0 for k == 0), saturation sums
+    int vpack;                 // low 16 bits (signed): Vi of v(k), -1 when v < black_thresh;
+                               // high 16 bits: gray group id of v(k)
+    int pad;
 };
 struct ClassTables {           // device copy, staged into LDS by the kernels
-    double rinv[256];          // 1 / k, k > 0  (saturation sums: s ~ (kmax-kmin)/kmax)
-    short vcol[256];           // Vi of v(kmax), or -1 when v < black_thresh
-    short vgray[256];          // gray group offset of v(kmax)
+    ClsEnt ent[256];
+    signed char si8[256 * 256];   // [kmax][kmax - kmin]: Si of s, -1 when s < gray_thresh
 };
 
 // Per-image device workspace views used by the palette kernels.
@@ -76,9 +77,19 @@ struct FftPlan {
 extern int g_ablate;   // ablation mask read by kernels under phd_debug_time_kernel
 int num_cus();         // compute units of the current device
 // hsv/stats/histogram pass over one image (K1).  ds = downsample rate.
-hipError_t launch_hsv_stats(const uint8_t* img, int height, int width, int ds,
-                            const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
-                            const PaletteDev& out, int nchunks, const double* k255, hipStream_t st);
+// K1 over a batch of same-size images (ds == 1); d_imgs is a device array of
+// n image pointers; image i's records sit at out0 + i * a_stride (sums, hist,
+// s_part) and out0.chunk_hist + i * h_stride bytes.  hist == false computes
+// only the moments and sum(s) (the rgb2hsv + statistics pass).  aligned: every
+// image pointer is 4-byte aligned (word loads; else byte loads).
+hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width,
+                                  const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
+                                  const PaletteDev& out0, long a_stride, long h_stride, int nchunks,
+                                  const double* k255, bool hist, bool aligned, hipStream_t st);
+// K1 for downsample_rate > 1 (one image).
+hipError_t launch_hsv_ds(const uint8_t* img, int height, int width, int ds, const GridParams& gp,
+                         const FastCls& fc, const ClassTables* tabs, const PaletteDev& out, int nchunks,
+                         const double* k255, hipStream_t st);
 // Locate the keep cutoff / last pixel for groups with rule.partial (Kcut).
 hipError_t launch_palette_cutoffs(const uint8_t* img, int height, int width, int ds,
                                   const GridParams& gp, const unsigned short* chunk_hist,

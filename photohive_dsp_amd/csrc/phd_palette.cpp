@@ -43,6 +43,7 @@ bool validate_config(const phd_config& c, std::string* why) {
     if (c.blur_cutoff_ratio_denom <= 0) return fail("blur_cutoff_ratio_denom must be positive");
     long tl = (long)c.h_partitions * c.s_partitions * c.v_partitions + c.v_partitions + 1;
     if (tl > 4096) return fail("h*s*v + v + 1 must be <= 4096 groups");
+    if (c.s_partitions > 127) return fail("s_partitions must be <= 127 (int8 saturation-class table)");
     return true;
 }
 
@@ -83,29 +84,27 @@ GroupCenters make_centers(const GridParams& g) {
 void make_class_tables(const GridParams& g, FastCls* fc, ClassTables* t) {
     // every entry is the reference's own double expression (rgb2hsv,
     // src/image_processing.c:388-414; arm_octree, src/color_quantization.c:131-145)
+    memset(t, 0, sizeof(*t));
     for (int k = 0; k < 256; k++) {
         const double v = (k == 255) ? 0.999999 : (double)k / 255.0;
-        t->rinv[k] = k ? 1.0 / (double)k : 0.0;
-        if (v < g.bt) {
-            t->vcol[k] = -1;
-            t->vgray[k] = 0;
-        } else {
-            t->vcol[k] = (short)(int)((v - g.bt) / g.Lv);
-            t->vgray[k] = (short)(int)((double)((int)(v - g.bt) * g.ng) / (1 - g.bt));
+        ClsEnt& e = t->ent[k];
+        e.rinv = k ? 1.0 / (double)k : 0.0;
+        int vcol = -1, vgray = 0;
+        if (v >= g.bt) {
+            vcol = (int)((v - g.bt) / g.Lv);
+            vgray = (int)((double)((int)(v - g.bt) * g.ng) / (1 - g.bt));
+        }
+        const int gray_id = g.tl - (g.ng + 1) + vgray;
+        e.vpack = (int)(((unsigned)gray_id << 16) | ((unsigned)vcol & 0xFFFFu));
+        // Si for every min <= max: s = max == 0 ? 0 : (d == max ? 0.999999 : d / max)
+        const double mx = (double)k / 255.0;
+        for (int kd = 0; kd <= k; kd++) {
+            const double mn = (double)(k - kd) / 255.0, d = mx - mn;
+            const double s = mx == 0 ? 0.0 : (d == mx ? 0.999999 : d / mx);
+            t->si8[k * 256 + kd] = (signed char)(s < g.gt ? -1 : (int)((s - g.gt) / g.Ls));
         }
     }
-    auto s_class = [&](double s) { return s < g.gt ? -1 : (int)((s - g.gt) / g.Ls); };
-    fc->si_full = s_class(0.999999);
-    fc->si_zero = s_class(0.0);
-    const double hx[9] = {0, 60, 300, 120, 180, 60, 240, 300, 180};   // quotient 0, +1, -1 per max channel
-    for (int i = 0; i < 9; i++) fc->hx[i] = (int)(hx[i] / g.Lh);
-    fc->gt = (float)g.gt;
-    fc->inv_ls = (float)(1.0 / g.Ls);
-    fc->inv_lh = (float)(1.0 / g.Lh);
-    // guard bands (in bins) well above the fp32 error bound of each quotient
-    fc->guard_s = (float)(3e-4 + 1e-6 / g.Ls + 2e-7 * g.sp);
-    fc->guard_h = 3e-4f;
-    fc->gray_base = g.tl - (g.ng + 1);
+    fc->lh = 360 / g.hp;
 }
 
 namespace {

@@ -34,11 +34,14 @@ struct Layout {
     size_t c_bins, c_fmax, c_pal, c_sharp, c_bytes;         // read back at the end (zeroed)
     size_t b_rules, b_search, b_off, b_bytes;               // uploaded before K3
     size_t chunk_bytes;                                      // device only
+    size_t ptr_bytes;                                        // image pointer array (pinned -> device)
     size_t dev_total, pin_total;
     size_t A(int i) const { return (size_t)i * a_bytes; }
     size_t C(int n, int i) const { return (size_t)n * a_bytes + (size_t)i * c_bytes; }
     size_t B(int n, int i) const { return (size_t)n * (a_bytes + c_bytes) + (size_t)i * b_bytes; }
     size_t H(int n, int i) const { return (size_t)n * (a_bytes + c_bytes + b_bytes) + (size_t)i * chunk_bytes; }
+    size_t P_dev(int n) const { return (size_t)n * (a_bytes + c_bytes + b_bytes + chunk_bytes); }
+    size_t P_pin(int n) const { return (size_t)n * (a_bytes + c_bytes + b_bytes); }
 };
 
 Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolblocks) {
@@ -57,8 +60,9 @@ Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolbl
     L.b_off = L.b_search + al(sizeof(int) * tl);
     L.b_bytes = L.b_off + al(sizeof(double) * tl);
     L.chunk_bytes = al(sizeof(unsigned short) * (size_t)nchunks * tl);
-    L.dev_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes + L.chunk_bytes);
-    L.pin_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes);
+    L.ptr_bytes = al(sizeof(void*) * (size_t)n);
+    L.dev_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes + L.chunk_bytes) + L.ptr_bytes;
+    L.pin_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes) + L.ptr_bytes;
     return L;
 }
 
@@ -213,6 +217,44 @@ RGB_Statistics stats_from_sums(const unsigned long long* m, long n) {
 
 }  // namespace
 
+bool all_aligned(const uint8_t* const* p, int n) {
+    for (int i = 0; i < n; i++)
+        if (reinterpret_cast<uintptr_t>(p[i]) & 3) return false;
+    return true;
+}
+
+// K1 for n same-size images: one batched launch (ds == 1) over the device
+// pointer array staged in the workspace, or per-image launches (ds > 1).
+bool launch_k1(Context* c, const Layout& L, int n, const uint8_t* const* d_imgs, int height, int width, int ds,
+               const GridParams& gp, const Context::Cls* cls, int nchunks, hipStream_t st) {
+    uint8_t* dw = (uint8_t*)c->d_ws;
+    uint8_t* hp = (uint8_t*)c->h_pin;
+    PaletteDev pd;
+    pd.sums = (unsigned long long*)(dw + L.A(0) + L.a_sums);
+    pd.hist = (unsigned*)(dw + L.A(0) + L.a_hist);
+    pd.s_part = (double*)(dw + L.A(0) + L.a_spart);
+    pd.chunk_hist = (unsigned short*)(dw + L.H(n, 0));
+    const int ps = c->prof.begin(kK1, st);
+    if (ds <= 1) {
+        memcpy(hp + L.P_pin(n), d_imgs, sizeof(void*) * n);
+        PHD_HIP(hipMemcpyAsync(dw + L.P_dev(n), hp + L.P_pin(n), sizeof(void*) * n, hipMemcpyHostToDevice, st));
+        PHD_HIP(launch_hsv_stats_batch((const uint8_t* const*)(dw + L.P_dev(n)), n, height, width, gp, cls->fc,
+                                       cls->d, pd, (long)L.a_bytes, (long)L.chunk_bytes, nchunks, c->d_k255,
+                                       true, all_aligned(d_imgs, n), st));
+    } else {
+        for (int i = 0; i < n; i++) {
+            PaletteDev pi;
+            pi.sums = (unsigned long long*)(dw + L.A(i) + L.a_sums);
+            pi.hist = (unsigned*)(dw + L.A(i) + L.a_hist);
+            pi.s_part = (double*)(dw + L.A(i) + L.a_spart);
+            pi.chunk_hist = (unsigned short*)(dw + L.H(n, i));
+            PHD_HIP(launch_hsv_ds(d_imgs[i], height, width, ds, gp, cls->fc, cls->d, pi, nchunks, c->d_k255, st));
+        }
+    }
+    c->prof.end(ps, st);
+    return true;
+}
+
 bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, int width,
                  const phd_config& cfg, const Crop_Boundaries* crops, Full_Report_Data** out, int* status,
                  hipStream_t stream) {
@@ -268,16 +310,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
 
     PHD_HIP(hipMemsetAsync(dw, 0, (size_t)n * (L.a_bytes + L.c_bytes), st));
     PHD_HIP(hipEventRecord(c->ev[0], st));
-    for (int i = 0; i < n; i++) {
-        PaletteDev pd;
-        pd.sums = (unsigned long long*)(dw + L.A(i) + L.a_sums);
-        pd.hist = (unsigned*)(dw + L.A(i) + L.a_hist);
-        pd.s_part = (double*)(dw + L.A(i) + L.a_spart);
-        pd.chunk_hist = (unsigned short*)(dw + L.H(n, i));
-        const int ps = c->prof.begin(kK1, st);
-        PHD_HIP(launch_hsv_stats(d_imgs[i], height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st));
-        c->prof.end(ps, st);
-    }
+    if (!launch_k1(c, L, n, d_imgs, height, width, ds, gp, cls, nchunks, st)) return false;
     PHD_HIP(hipEventRecord(c->ev[1], st));
     PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipEventRecord(c->ev[5], st));
@@ -311,12 +344,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             ok[i] = 0;
             continue;
         }
-        uint8_t* b = hp + L.pin_total - (size_t)n * L.b_bytes + (size_t)i * L.b_bytes;
+        uint8_t* b = hp + (size_t)n * (L.a_bytes + L.c_bytes) + (size_t)i * L.b_bytes;
         memcpy(b + L.b_rules, dec[i].rules.data(), sizeof(GroupRule) * gp.tl);
         memcpy(b + L.b_search, dec[i].search.data(), sizeof(int) * dec[i].search.size());
         memcpy(b + L.b_off, dec[i].off.data(), sizeof(double) * dec[i].off.size());
     }
-    uint8_t* hb = hp + L.pin_total - (size_t)n * L.b_bytes;
+    uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
     PHD_HIP(hipMemcpyAsync(dw + L.B(n, 0), hb, (size_t)n * L.b_bytes, hipMemcpyHostToDevice, st));
     for (int i = 0; i < n; i++) {
         if (!ok[i]) continue;
@@ -402,7 +435,7 @@ bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, 
     pd.chunk_hist = (unsigned short*)(dw + L.H(1, 0));
     const Context::Cls* cls = get_cls(c, gp);
     if (!cls) return false;
-    PHD_HIP(launch_hsv_stats(d_img, height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st));
+    if (!launch_k1(c, L, 1, &d_img, height, width, ds, gp, cls, nchunks, st)) return false;
     PHD_HIP(hipMemcpyAsync(hp, dw, L.a_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipStreamSynchronize(st));
     hist->assign((const unsigned*)(hp + L.a_hist), (const unsigned*)(hp + L.a_hist) + gp.tl);
@@ -581,6 +614,66 @@ extern "C" int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int h
     return fails;
 }
 
+// rgb2hsv + get_hsv_average + get_rgb_statistics (src/image_processing.c:372-417,
+// 533-553) over a batch of device images: one K1 launch without the group
+// histogram.  HSV is never materialised; S-bar is the mean of the HSV s channel.
+extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
+                                          size_t image_stride, RGB_Statistics* stats, double* avg_saturation,
+                                          void* stream) {
+    clear_error();
+    if (!d_rgb || !stats || !avg_saturation || n_images <= 0 || height <= 0 || width <= 0 ||
+        height > 32767 || width > 32767) {
+        set_error("phd_hsv_stats_batch_device: bad arguments");
+        return -1;
+    }
+    Context* c = get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
+    const long npix = (long)height * width;
+    const int nchunks = (int)((npix + kChunk - 1) / kChunk);
+    const size_t a_stride = al(6 * sizeof(unsigned long long)) + al(sizeof(double) * nchunks);
+    const size_t rec = (size_t)n_images * a_stride, ptrs = al(sizeof(void*) * (size_t)n_images);
+    if (!ensure_device(&c->d_ws, &c->ws_bytes, rec + ptrs) || !ensure_pinned(c, rec + ptrs)) return -1;
+    uint8_t* dw = (uint8_t*)c->d_ws;
+    uint8_t* hp = (uint8_t*)c->h_pin;
+    const uint8_t** hptr = (const uint8_t**)(hp + rec);
+    for (int i = 0; i < n_images; i++) hptr[i] = d_rgb + (size_t)i * stride;
+    const GridParams gp = make_grid([] { phd_config d; phd_config_default(&d); return d; }());
+    const Context::Cls* cls = get_cls(c, gp);
+    if (!cls) return -1;
+    PaletteDev pd{};
+    pd.sums = (unsigned long long*)dw;
+    pd.s_part = (double*)(dw + al(6 * sizeof(unsigned long long)));
+    auto fail = [&](hipError_t e, const char* what) {
+        set_error(std::string("phd_hsv_stats_batch_device: ") + what + ": " + hipGetErrorString(e));
+        return -1;
+    };
+    hipError_t e;
+    if ((e = hipMemsetAsync(dw, 0, rec, st)) != hipSuccess) return fail(e, "memset");
+    if ((e = hipMemcpyAsync(dw + rec, hptr, sizeof(void*) * n_images, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return fail(e, "pointer upload");
+    const int ps = c->prof.begin(kK1, st);
+    if ((e = launch_hsv_stats_batch((const uint8_t* const*)(dw + rec), n_images, height, width, gp, cls->fc,
+                                    cls->d, pd, (long)a_stride, 0, nchunks, c->d_k255, false,
+                                    all_aligned(hptr, n_images), st)) != hipSuccess)
+        return fail(e, "launch");
+    c->prof.end(ps, st);
+    if ((e = hipMemcpyAsync(hp, dw, rec, hipMemcpyDeviceToHost, st)) != hipSuccess) return fail(e, "readback");
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return fail(e, "sync");
+    c->prof.collect();
+    for (int i = 0; i < n_images; i++) {
+        const uint8_t* a = hp + (size_t)i * a_stride;
+        stats[i] = stats_from_sums((const unsigned long long*)a, npix);
+        const double* sp = (const double*)(a + al(6 * sizeof(unsigned long long)));
+        double sacc = 0.0;
+        for (int k = 0; k < nchunks; k++) sacc += sp[k];
+        avg_saturation[i] = sacc / (double)npix;
+    }
+    return 0;
+}
+
 extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
                                    int n_images, const phd_config* cfg, Full_Report_Data** out, int* status) {
     clear_error();
@@ -707,6 +800,10 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
     pd.hist = (unsigned*)(dw + 256);
     pd.s_part = (double*)(dw + 256 + 4 * 4096);
     pd.chunk_hist = (unsigned short*)(dw + 256 + 4 * 4096 + 8 * (size_t)nchunks);
+    const uint8_t** d_ptr = nullptr;
+    if (!ensure_device((void**)&c->d_ptrs, &c->ptrs_bytes, sizeof(void*))) return -1;
+    d_ptr = (const uint8_t**)c->d_ptrs;
+    if (hipMemcpy(d_ptr, &d_rgb, sizeof(void*), hipMemcpyHostToDevice) != hipSuccess) return -1;
     g_ablate = ablate;
     const hipStream_t st = c->stream;
     hipEvent_t a = c->ev[6], b = c->ev[7];
@@ -714,7 +811,12 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
         if (it == 0) (void)hipEventRecord(a, st);
         hipError_t e = hipSuccess;
         switch (kernel) {
-            case kK1: e = launch_hsv_stats(d_rgb, height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st); break;
+            case kK1:
+            case kNumKernels:   // K1 without the group histogram (the rgb2hsv + statistics pass)
+                e = ds > 1 ? launch_hsv_ds(d_rgb, height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st)
+                           : launch_hsv_stats_batch(d_ptr, 1, height, width, gp, cls->fc, cls->d, pd, 0, 0, nchunks,
+                                                    c->d_k255, kernel == kK1, all_aligned(&d_rgb, 1), st);
+                break;
             case kFftRows: e = launch_fft_rows(d_rgb, height, width, prow->plan, pd.sums, c->d_k255, c->d_inter, st); break;
             case kFftCols: e = launch_fft_cols(c->d_inter, height, wf, pcol->plan, tbl->d_map,
                                                cfg->radius_partitions * cfg->angle_partitions, (double*)pd.chunk_hist,

@@ -4,7 +4,7 @@ import ctypes
 import os
 
 from .structures import (Blur_Profile, Crop_Boundaries, Full_Report_Data, Image_PGM, Image_RGB,
-                         PhdConfig)
+                         PhdConfig, RGB_Statistics)
 
 def _preload_torch_hip_runtime():
     """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64.so
@@ -24,6 +24,8 @@ def _preload_torch_hip_runtime():
 _preload_torch_hip_runtime()
 directory = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.path.join(directory, "PhotoHive_DSP_lib/libreport_data.so")
+if os.environ.get("PHD_LIB"):          # kernel-variant experiments (tools/); not for production
+    lib_path = os.path.abspath(os.environ["PHD_LIB"])
 if not os.path.exists(lib_path):
     raise ImportError(f"{lib_path} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                       "or `make -C photohive_dsp_amd/csrc` (there is no CPU fallback)")
@@ -52,6 +54,10 @@ lib.phd_report_batch_device.restype = ctypes.c_int
 lib.phd_report_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_size_t, P(PhdConfig), P(P(Full_Report_Data)),
                                         P(ctypes.c_int), ctypes.c_void_p]
+lib.phd_hsv_stats_batch_device.restype = ctypes.c_int
+lib.phd_hsv_stats_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_size_t, P(RGB_Statistics), P(ctypes.c_double),
+                                           ctypes.c_void_p]
 lib.phd_report_batch_u8.restype = ctypes.c_int
 lib.phd_report_batch_u8.argtypes = [P(ctypes.c_void_p), P(ctypes.c_int), P(ctypes.c_int), ctypes.c_int,
                                     P(PhdConfig), P(P(Full_Report_Data)), P(ctypes.c_int)]

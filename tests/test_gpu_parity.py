@@ -136,6 +136,52 @@ def test_batch_device_matches_single_reports():
                                    atol=1e-14)
 
 
+def test_batched_k1_runs_cross_images():
+    """One K1 launch over 12 images (576 chunk items > one item per block, so block runs
+    cross image boundaries): every image's palette and statistics equal the oracle's."""
+    phd, L, torch = _phd()
+    from oracle import oracle as orc
+    from photohive_dsp_amd import synth
+    h, w, n = 768, 1024, 12
+    t = torch.empty(n * h * w * 3, dtype=torch.uint8, device="cuda")
+    for i in range(n):
+        assert L.lib.phd_fill_uniform_device(t[i * h * w * 3:].data_ptr(), h * w * 3, 100 + i, None) == 0
+    reps = phd.report_device(t.view(n, h, w, 3))
+    for i, r in enumerate(reps):
+        img = synth.uniform(h, w, 100 + i)
+        o = orc.palette(img)
+        np.testing.assert_array_equal(np.array(r.color_palette.group_ids), o["valid_parents"])
+        np.testing.assert_array_equal(np.array(r.color_palette.quantities), o["palette_pct"])
+        st = r.rgb_stats
+        np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], orc.stats(img), rtol=TIGHT_RTOL)
+        np.testing.assert_allclose(r.average_saturation, o["average_saturation"], rtol=TIGHT_RTOL)
+
+
+def test_hsv_stats_batch_config3_shape():
+    """BASELINE config 3 pass (rgb2hsv + get_hsv_average + get_rgb_statistics) over a batch of
+    1080p device images against the oracle."""
+    phd, L, torch = _phd()
+    from oracle import oracle as orc
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import hsv_stats_device
+    h, w, n = 1080, 1920, 20
+    t = torch.empty(n * h * w * 3, dtype=torch.uint8, device="cuda")
+    for i in range(n):
+        assert L.lib.phd_fill_uniform_device(t[i * h * w * 3:].data_ptr(), h * w * 3, i, None) == 0
+    stats, sat = hsv_stats_device(t.view(n, h, w, 3))
+    for i in (0, 1, 9, 19):
+        img = synth.uniform(h, w, i)
+        st = stats[i]
+        np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], orc.stats(img), rtol=TIGHT_RTOL)
+        np.testing.assert_allclose(sat[i], orc.palette(img)["average_saturation"], rtol=TIGHT_RTOL)
+    # a structured image (flat regions) in a batch of one
+    img = synth.make("structured", h, w, 5)
+    stats, sat = hsv_stats_device(torch.from_numpy(img[None]).cuda())
+    st = stats[0]
+    np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], orc.stats(img), rtol=TIGHT_RTOL)
+    np.testing.assert_allclose(sat[0], orc.palette(img)["average_saturation"], rtol=TIGHT_RTOL)
+
+
 def test_mixed_size_host_batch():
     phd, L, _ = _phd()
     from photohive_dsp_amd import synth
