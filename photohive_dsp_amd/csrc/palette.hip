@@ -92,7 +92,10 @@ __device__ __forceinline__ void hist_add(unsigned* lds, int g) {
 }
 
 #ifndef PHD_K1_ABLATE
-#define PHD_K1_ABLATE 0        // K1 ablation mask for timing builds (16 hist, 32 sat, 128 atomics)
+#define PHD_K1_ABLATE 0        // K1 ablation mask for timing builds (8 classify, 16 hist, 32 sat, 128 atomics)
+#endif
+#ifndef PHD_SAT_MODE
+#define PHD_SAT_MODE 0
 #endif
 #ifndef PHD_K1_MINWAVES
 #define PHD_K1_MINWAVES 8        // waves/SIMD the statistics-only K1 is sized for (2 blocks/CU)
@@ -190,6 +193,8 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
     stage_tables(smem, k255g, tabs, kHist);
+    if (!kHist && PHD_SAT_MODE == 1 && tid < 256) reinterpret_cast<double*>(smem + K1Lds::si8)[tid] = tabs->ent[tid].rinv;
+    if (!kHist && PHD_SAT_MODE == 2 && tid < 256) reinterpret_cast<float*>(smem + K1Lds::si8)[tid] = (float)tabs->ent[tid].rinv;
     if (kHist) {
         for (int i = tid; i < 2 * tl1 + tl; i += kK1Threads) lh[i] = 0;
         if (tid < 2) qn[tid] = 0;
@@ -231,14 +236,15 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
         for (int st = 0; st < kSteps; st++) {
             const int o0 = 4 * tid + 4 * kK1Threads * st;     // offset in the chunk
             const unsigned cw[3] = {c0, c1, c2};
+            float s4 = 0.f;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int kr = px_byte(cw, 3 * i), kg = px_byte(cw, 3 * i + 1), kb = px_byte(cw, 3 * i + 2);
                 sr += kr; sg += kg; sb += kb;
                 qr += kr * kr; qg += kg * kg; qb += kb * kb;
                 if (kHist) {
-                    double sv;
-                    int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+                    double sv = 0.0;
+                    int g = (ablate & 8) ? (kr & 63) : classify(kr, kg, kb, ent, si8, gp, fc, sv);
                     if (!(ablate & 32)) ssum += sv;
                     if (g == -2) {            // on a hue bin edge: classify exactly after the stream
                         queue[atomicAdd(&qn[par], 1)] = (unsigned short)(o0 + i);
@@ -246,9 +252,33 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
                     }
                     if (!(ablate & 16)) hist_add_full(ch, g);
                 } else {
+#if PHD_SAT_MODE == 0
                     if (!(ablate & 32)) ssum += sat_only(kr, kg, kb, ent);
+#elif PHD_SAT_MODE == 1
+                    {
+                        const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
+                        const double sv = (double)kd * reinterpret_cast<const double*>(si8)[kmx];
+                        ssum += (kmn == 0 && kd != 0) ? 0.999999 : sv;
+                    }
+#elif PHD_SAT_MODE == 2
+                    {
+                        const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
+                        const float sv = (float)kd * reinterpret_cast<const float*>(si8)[kmx];
+                        s4 += (kmn == 0 && kd != 0) ? 0.999999f : sv;
+                    }
+#else
+                    {
+                        const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
+                        const double k = (double)max(kmx, 1);
+                        double r = __builtin_amdgcn_rcp(k);
+                        r = fma(fma(-k, r, 1.0), r, r);
+                        const double sv = (double)kd * r;
+                        ssum += (kmn == 0 && kd != 0) ? 0.999999 : sv;
+                    }
+#endif
                 }
             }
+            if (PHD_SAT_MODE == 2) ssum += (double)s4;
             bits >>= 1;
             const bool okn = bits & 1;
             c0 = okn ? w[1][0] : 0u;
@@ -353,6 +383,316 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
             seg_c0 = c;
             seg_it0 = it + 1;
             __syncthreads();                                  // red is reused by the next flush
+        }
+    }
+}
+
+// Exclusive scan of one int per thread over a block of kK1Threads threads.
+__device__ int block_excl_scan_k1(int x, int& excl, int* scratch) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    int incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) scratch[w] = incl;
+    __syncthreads();
+    int wpre = 0, tot = 0;
+    for (int q = 0; q < kK1Threads / 64; q++) {
+        if (q < w) wpre += scratch[q];
+        tot += scratch[q];
+    }
+    __syncthreads();
+    excl = wpre + incl - x;
+    return tot;
+}
+
+// The same for a u64 (packed per-step counts).
+__device__ unsigned long long block_excl_scan_k1_u64(unsigned long long x, unsigned long long& excl,
+                                                     unsigned long long* scratch) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    unsigned long long incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) scratch[w] = incl;
+    __syncthreads();
+    unsigned long long wpre = 0, tot = 0;
+    for (int q = 0; q < kK1Threads / 64; q++) {
+        if (q < w) wpre += scratch[q];
+        tot += scratch[q];
+    }
+    __syncthreads();
+    excl = wpre + incl - x;
+    return tot;
+}
+
+// Exact group of a pixel: classify(), and the exact hue on a bin edge.
+__device__ __forceinline__ int exact_group_t(int kr, int kg, int kb, const ClsEnt* ent, const signed char* si8,
+                                             const double* k255, const GridParams& gp, const FastCls& fc,
+                                             double& s) {
+    int g = classify(kr, kg, kb, ent, si8, gp, fc, s);
+    if (g == -2) g = edge_group(kr, kg, kb, hue_exact(kr, kg, kb, k255), ent, si8, gp);
+    return g;
+}
+
+// Kcut for downsample_rate == 1, all images of a batch in one launch: one block
+// per (image, group) whose keep rule needs raster positions (the tie path of
+// group_irregular_pixels appends pixels in raster order until the parent's tail
+// node is full, src/color_quantization.c:435-440): the index of the group's
+// keep-th pixel (cutoff = index + 1) and of its last pixel (the dangling
+// node).  The per-chunk counts of K1 locate the chunk; one pass over that
+// chunk's 16384 pixels (16 per thread) and a block scan find the pixel.
+template <bool kAligned>
+__global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
+        const uint8_t* const* __restrict__ imgs, long npix, int nchunks, GridParams gp, FastCls fc,
+        const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, const int2* __restrict__ entries,
+        const unsigned short* __restrict__ chunk_hist0, long h_stride, GroupRule* rules0, long b_stride) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
+    const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
+    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
+    int* scratch = reinterpret_cast<int*>(smem + K1Lds::red);          // 16 x u64
+    int* misc = reinterpret_cast<int*>(smem + K1Lds::red + 256);       // chunk, rank, last chunk
+    unsigned* found = reinterpret_cast<unsigned*>(smem + K1Lds::qn);
+    const int tid = threadIdx.x;
+    stage_tables(smem, k255g, tabs, true);
+    const int img = entries[blockIdx.x].x, g = entries[blockIdx.x].y;
+    const uint8_t* ip = imgs[img];
+    GroupRule* rules = reinterpret_cast<GroupRule*>(reinterpret_cast<char*>(rules0) + img * b_stride);
+    const unsigned short* chunk_hist =
+            reinterpret_cast<const unsigned short*>(reinterpret_cast<const char*>(chunk_hist0) + img * h_stride);
+    const int tl = gp.tl;
+    const int keep = rules[g].keep;
+    const bool want_cut = rules[g].partial && keep > 0;
+    const bool want_last = rules[g].partial && rules[g].dangle;
+    if (tid == 0) { misc[0] = -1; misc[2] = -1; }
+    __syncthreads();
+    // chunk holding the keep-th pixel, and the last non-empty chunk
+    int carry = 0;
+    for (int c0 = 0; c0 < nchunks; c0 += kK1Threads) {
+        const int c = c0 + tid;
+        const int cnt = c < nchunks ? (int)chunk_hist[(long)c * tl + g] : 0;
+        int excl;
+        const int tot = block_excl_scan_k1(cnt, excl, scratch);
+        if (want_cut && cnt > 0 && carry + excl < keep && keep <= carry + excl + cnt) {
+            misc[0] = c;
+            misc[1] = keep - (carry + excl);   // 1-based rank inside the chunk
+        }
+        if (cnt > 0) atomicMax(&misc[2], c);
+        carry += tot;
+    }
+    __syncthreads();
+    constexpr int kSteps = kChunk / (4 * kK1Threads);
+    const long full_end = npix & ~3L;
+    for (int pass = 0; pass < 2; pass++) {
+        const int c = pass == 0 ? (want_cut ? misc[0] : -1) : (want_last ? misc[2] : -1);
+        if (c < 0) continue;                                  // uniform across the block
+        // this thread's 16 pixels: hit bits in raster order
+        unsigned hits = 0;
+#pragma unroll
+        for (int st = 0; st < kSteps; st++) {
+            const long p0 = (long)c * kChunk + 4L * tid + 4L * kK1Threads * st;
+            unsigned w[3];
+            load_group<kAligned>(ip, p0, p0 < full_end, w);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const long p = p0 + i;
+                int kr, kg, kb;
+                if (p0 < full_end) {
+                    kr = px_byte(w, 3 * i); kg = px_byte(w, 3 * i + 1); kb = px_byte(w, 3 * i + 2);
+                } else if (p < npix) {                        // partial final group
+                    kr = ip[3 * p]; kg = ip[3 * p + 1]; kb = ip[3 * p + 2];
+                } else {
+                    continue;
+                }
+                double sv;
+                if (exact_group_t(kr, kg, kb, ent, si8, k255, gp, fc, sv) == g) hits |= 1u << (4 * st + i);
+            }
+        }
+        if (tid == 0) *found = 0;
+        // raster order inside the chunk is (step, thread, pixel): scan the
+        // per-step hit counts (4 x 16-bit fields) over the threads
+        unsigned long long packed = 0;
+#pragma unroll
+        for (int st = 0; st < kSteps; st++)
+            packed |= (unsigned long long)__popc((hits >> (4 * st)) & 15u) << (16 * st);
+        unsigned long long excl;
+        const unsigned long long tot =
+                block_excl_scan_k1_u64(packed, excl, reinterpret_cast<unsigned long long*>(scratch));
+        if (pass == 0) {
+            const int rank = misc[1];
+            int before = 0;                                   // hits of the earlier steps
+#pragma unroll
+            for (int st = 0; st < kSteps; st++) {
+                const int e = before + (int)((excl >> (16 * st)) & 0xFFFF);
+                const int n = (int)((packed >> (16 * st)) & 0xFFFF);
+                if (e < rank && rank <= e + n) {
+                    unsigned m = (hits >> (4 * st)) & 15u;
+                    for (int k = rank - e; k > 1; k--) m &= m - 1;   // drop the lower hits
+                    const int i = __ffs(m) - 1;
+                    *found = (unsigned)((long)c * kChunk + 4L * tid + 4L * kK1Threads * st + i) + 1;
+                }
+                before += (int)((tot >> (16 * st)) & 0xFFFF);
+            }
+        } else if (hits) {
+            const int b = 31 - __clz(hits);
+            atomicMax(found, (unsigned)((long)c * kChunk + 4L * tid + 4L * kK1Threads * (b >> 2) + (b & 3)) + 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (pass == 0) rules[g].cutoff = *found;          // index + 1 of the keep-th pixel
+            else rules[g].last = *found - 1;
+        }
+        __syncthreads();
+    }
+}
+
+// K3 for downsample_rate == 1, all images of a batch in one launch: per palette
+// slot, over the pixels its parent keeps (calculate_avg_hsv,
+// src/color_quantization.c:529-558): sum wrap(h + off), sum s, sum v, count.
+// Persistent blocks walk contiguous runs of (image, chunk) items like K1;
+// per image the keep rules are packed into LDS as {slot, cut, last}: a pixel
+// of a slotted group is kept when its index < cut or == last.  Sums stay in
+// LDS per slot and go to HBM with one atomic per slot and field per run.
+template <bool kAligned>
+__global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
+        const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
+        const ClassTables* __restrict__ tabs, const double* __restrict__ k255g,
+        const GroupRule* __restrict__ rules0, const double* __restrict__ off0, long b_stride,
+        const int* __restrict__ nslots_img, int max_slots, double* out0, long c_stride) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
+    const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
+    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
+    const int tl = gp.tl;
+    uint4* rec = reinterpret_cast<uint4*>(smem + K1Lds::queue);        // [tl] {slot, cut, last, -}
+    double* off = reinterpret_cast<double*>(rec + tl);                 // [max_slots]
+    double* acc = off + max_slots;                                     // [3][max_slots] h, s, v
+    unsigned* cnt = reinterpret_cast<unsigned*>(acc + 3 * max_slots);  // [max_slots]
+    const int tid = threadIdx.x;
+    const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
+    if (it0 >= it1) return;                                 // block-uniform
+    stage_tables(smem, k255g, tabs, true);
+
+    constexpr int kSteps = kChunk / (4 * kK1Threads);
+    const long full_end = npix & ~3L;
+    int img = (int)(it0 / nchunks), c = (int)(it0 - (long)img * nchunks);
+    int cur = -1, ns = 0;
+    for (long it = it0; it < it1; it++) {
+        if (img != cur) {                                    // block-uniform: load image img's rules
+            const GroupRule* rules =
+                    reinterpret_cast<const GroupRule*>(reinterpret_cast<const char*>(rules0) + img * b_stride);
+            const double* offi = reinterpret_cast<const double*>(reinterpret_cast<const char*>(off0) + img * b_stride);
+            ns = nslots_img[img];
+            for (int i = tid; i < tl; i += kK1Threads) {
+                const GroupRule r = rules[i];
+                uint4 q;
+                q.x = (unsigned)r.slot;
+                q.y = r.partial ? r.cutoff : 0xFFFFFFFFu;
+                q.z = (r.partial && r.dangle) ? r.last : 0xFFFFFFFFu;
+                q.w = 0;
+                rec[i] = q;
+            }
+            for (int i = tid; i < ns; i += kK1Threads) {
+                off[i] = offi[i];
+                acc[i] = acc[max_slots + i] = acc[2 * max_slots + i] = 0.0;
+                cnt[i] = 0;
+            }
+            cur = img;
+            __syncthreads();
+        }
+        const uint8_t* ip = imgs[img];
+        const long base = (long)c * kChunk;
+        unsigned w[kSteps][3];
+#pragma unroll
+        for (int st = 0; st < kSteps; st++) {
+            const long p0 = base + 4L * tid + 4L * kK1Threads * st;
+            load_group<kAligned>(ip, p0, p0 < full_end, w[st]);
+        }
+#pragma unroll 1
+        for (int st = 0; st < kSteps; st++) {
+            const long p0 = base + 4L * tid + 4L * kK1Threads * st;
+            const bool okg = p0 < full_end;
+            unsigned cw[3];
+#pragma unroll
+            for (int k = 0; k < kSteps; k++)
+                if (k == st) { cw[0] = w[k][0]; cw[1] = w[k][1]; cw[2] = w[k][2]; }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int kr = px_byte(cw, 3 * i), kg = px_byte(cw, 3 * i + 1), kb = px_byte(cw, 3 * i + 2);
+                double sv;
+                int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+                const double hx = hue_exact(kr, kg, kb, k255);
+                if (g == -2) g = edge_group(kr, kg, kb, hx, ent, si8, gp);
+                const uint4 q = rec[g];
+                const unsigned idx = (unsigned)(p0 + i);
+                const bool kept = okg && (int)q.x >= 0 && (idx < q.y || idx == q.z);
+                const int sl = kept ? (int)q.x : -1;
+                double tp = hx + off[kept ? sl : 0];
+                tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+                const double vv = v_of(max(kr, max(kg, kb)), k255);
+                const int s0 = __builtin_amdgcn_readfirstlane(sl);
+                if (__builtin_amdgcn_ballot_w64(sl != s0) == 0) {
+                    if (s0 >= 0) {
+                        const double th = wave_sum(tp), ts = wave_sum(sv), tv = wave_sum(vv);
+                        if (lane_id() == 0) {
+                            atomicAdd(&acc[s0], th);
+                            atomicAdd(&acc[max_slots + s0], ts);
+                            atomicAdd(&acc[2 * max_slots + s0], tv);
+                            atomicAdd(&cnt[s0], 64u);
+                        }
+                    }
+                } else if (sl >= 0) {
+                    atomicAdd(&acc[sl], tp);
+                    atomicAdd(&acc[max_slots + sl], sv);
+                    atomicAdd(&acc[2 * max_slots + sl], vv);
+                    atomicAdd(&cnt[sl], 1u);
+                }
+            }
+        }
+        if (base + kChunk >= npix && tid == 0) {
+            // the partial final group of the image: one lane, plain atomics
+            for (long p = full_end; p < npix; p++) {
+                const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
+                double sv;
+                const double hx = hue_exact(kr, kg, kb, k255);
+                int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+                if (g == -2) g = edge_group(kr, kg, kb, hx, ent, si8, gp);
+                const uint4 q = rec[g];
+                const unsigned idx = (unsigned)p;
+                if ((int)q.x >= 0 && (idx < q.y || idx == q.z)) {
+                    const int sl = (int)q.x;
+                    double tp = hx + off[sl];
+                    tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+                    atomicAdd(&acc[sl], tp);
+                    atomicAdd(&acc[max_slots + sl], sv);
+                    atomicAdd(&acc[2 * max_slots + sl], v_of(max(kr, max(kg, kb)), k255));
+                    atomicAdd(&cnt[sl], 1u);
+                }
+            }
+        }
+        const int cimg = img;
+        if (++c == nchunks) {
+            c = 0;
+            img++;
+        }
+        if (it + 1 == it1 || img != cimg) {                  // flush image cimg's sums
+            __syncthreads();
+            double* out = reinterpret_cast<double*>(reinterpret_cast<char*>(out0) + cimg * c_stride);
+            for (int i = tid; i < ns; i += kK1Threads) {
+                const unsigned n = cnt[i];
+                if (n) {
+                    atomicAdd(&out[4 * i + 0], acc[i]);
+                    atomicAdd(&out[4 * i + 1], acc[max_slots + i]);
+                    atomicAdd(&out[4 * i + 2], acc[2 * max_slots + i]);
+                    atomicAdd(&out[4 * i + 3], (double)n);
+                }
+            }
+            __syncthreads();
         }
     }
 }
@@ -667,7 +1007,7 @@ static inline long hsv_pixels(int height, int width, int ds, int* nw) {
 }
 
 size_t hsv_stats_lds(const GridParams& gp, bool hist) {
-    return hist ? K1Lds::hist + sizeof(unsigned) * (3 * (size_t)gp.tl + 2) : (size_t)K1Lds::si8;
+    return hist ? K1Lds::hist + sizeof(unsigned) * (3 * (size_t)gp.tl + 2) : (size_t)K1Lds::si8 + 2048;
 }
 
 hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width,
@@ -742,6 +1082,68 @@ hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds
     const int aligned = (reinterpret_cast<uintptr_t>(img) & 3) == 0;
     hipLaunchKernelGGL(k_palette_sums, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw,
                        gp, rules, slot_off, nslots, out, k255, aligned);
+    return hipGetLastError();
+}
+
+size_t palette_sums_b_lds(int tl, int max_slots) {
+    return (size_t)K1Lds::queue + 16 * (size_t)tl + 36 * (size_t)max_slots;
+}
+
+hipError_t launch_cutoffs_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n, int height,
+                                int width, const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
+                                const double* k255, const int2* entries, int n_entries,
+                                const unsigned short* chunk_hist0, long h_stride, GroupRule* rules0,
+                                long b_stride, hipStream_t st) {
+    if (n_entries <= 0) return hipSuccess;
+    const long npix = (long)height * width;
+    const int nchunks = (int)((npix + kChunk - 1) / kChunk);
+    bool aligned = true;
+    for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
+    const size_t lds = K1Lds::queue;
+#define PHD_KCUT_LAUNCH(A)                                                                                  \
+    do {                                                                                                    \
+        static bool attr = false;                                                                           \
+        if (!attr) {                                                                                        \
+            (void)hipFuncSetAttribute((const void*)k_cutoffs_b<A>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                      160 * 1024);                                                          \
+            attr = true;                                                                                    \
+        }                                                                                                   \
+        hipLaunchKernelGGL((k_cutoffs_b<A>), dim3(n_entries), dim3(kK1Threads), lds, st, d_imgs, npix,        \
+                           nchunks, gp, fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, b_stride);  \
+    } while (0)
+    if (aligned) PHD_KCUT_LAUNCH(true);
+    else PHD_KCUT_LAUNCH(false);
+#undef PHD_KCUT_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n,
+                                     int height, int width, const GridParams& gp, const FastCls& fc,
+                                     const ClassTables* tabs, const double* k255, const GroupRule* rules0,
+                                     const double* off0, long b_stride, const int* nslots_img, int max_slots,
+                                     double* out0, long c_stride, hipStream_t st) {
+    const long npix = (long)height * width;
+    const int nchunks = (int)((npix + kChunk - 1) / kChunk);
+    const long nitems = (long)n * nchunks;
+    bool aligned = true;
+    for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
+    const size_t lds = palette_sums_b_lds(gp.tl, max_slots);
+    const int grid = (int)std::min<long>(nitems, num_cus());
+#define PHD_K3_LAUNCH(A)                                                                                    \
+    do {                                                                                                    \
+        static bool attr = false;                                                                           \
+        if (!attr) {                                                                                        \
+            (void)hipFuncSetAttribute((const void*)k_palette_sums_b<A>,                                     \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              \
+            attr = true;                                                                                    \
+        }                                                                                                   \
+        hipLaunchKernelGGL((k_palette_sums_b<A>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix,        \
+                           nchunks, nitems, gp, fc, tabs, k255, rules0, off0, b_stride, nslots_img,         \
+                           max_slots, out0, c_stride);                                                      \
+    } while (0)
+    if (aligned) PHD_K3_LAUNCH(true);
+    else PHD_K3_LAUNCH(false);
+#undef PHD_K3_LAUNCH
     return hipGetLastError();
 }
 

@@ -46,14 +46,6 @@ __device__ __forceinline__ int group_of(const GridParams& gp, double h, double s
     return (hi * gp.sp + si) * gp.vp + vi;
 }
 
-// Group id from integer facts and an fp32 estimate, or -2 when the pixel's
-// hue or saturation quotient lies within the guard band of a bin edge and must
-// take the exact path (rgb2hsv + group_of).  Away from the band the fp32 and
-// the reference's fp64 quotients truncate to the same integer: the fp32 error
-// is < 1e-4 of a bin while a non-integral hue quotient (base + 60 n/kd)/Lh with
-// Lh | 360 sits >= 1/(6 kd) >= 6.5e-4 from an integer.  Exact special cases:
-// v-classes come from a table over kmax; s == 0 (kd == 0) and s == 0.999999
-// (kmin == 0); hue quotients 0 and +-1 (num == 0, +-kd) are exact in fp64.
 // Group id of a pixel (or -2: take the exact path) and its HSV saturation.
 // Vi, the gray group and Si come from tables of the reference's own double
 // results; the hue bin is exact integer arithmetic: with N = 60*num + base*d
@@ -87,6 +79,35 @@ __device__ __forceinline__ int classify(int kr, int kg, int kb, const ClsEnt* en
     g = si < 0 ? gray : g;
     return vi < 0 ? gp.tl - 1 : g;
 }
+
+// rgb2hsv's hue, bit-exact (same doubles, same operation order), select-only:
+// the branch's channel difference over d, plus 0/2/4 sectors, times 60.
+__device__ __forceinline__ double hue_exact(int kr, int kg, int kb, const double* k255) {
+    const double r = k255[kr], g = k255[kg], b = k255[kb];
+    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
+    const double d = k255[kmx] - k255[kmn];
+    const bool isr = kr == kmx, isg = kg == kmx;
+    const double num = isr ? g - b : (isg ? b - r : r - g);
+    const double sector = isr ? 0.0 : (isg ? 2.0 : 4.0);
+    // 60 * (0 + q) == 60 * q exactly; d == 0 gives NaN here and is selected away
+    double h = 60 * (sector + num / d);
+    h = kmx == kmn ? 0.0 : h;
+    return h < 0 ? h + 360 : h;
+}
+
+// The group of a pixel that classify() left on a hue bin edge (-2: a colour
+// pixel), from its exact hue: arm_octree's (int)(h / Lh).
+__device__ __forceinline__ int edge_group(int kr, int kg, int kb, double h, const ClsEnt* ent,
+                                          const signed char* si8, const GridParams& gp) {
+    const int kmx = max(kr, max(kg, kb)), kd = kmx - min(kr, min(kg, kb));
+    const int si = si8[(kmx << 8) | kd];
+    const int vi = (ent[kmx].vpack << 16) >> 16;
+    const int hi = (int)(h / gp.Lh);
+    return (hi * gp.sp + si) * gp.vp + vi;
+}
+
+// v of rgb2hsv for max channel value k: k/255, 0.999999 for 255.
+__device__ __forceinline__ double v_of(int kmx, const double* k255) { return kmx == 255 ? 0.999999 : k255[kmx]; }
 
 // HSV saturation alone (rgb2hsv's s), for the statistics-only pass.
 __device__ __forceinline__ double sat_only(int kr, int kg, int kb, const ClsEnt* ent) {

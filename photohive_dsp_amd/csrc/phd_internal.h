@@ -86,6 +86,21 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
                                   const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
                                   const PaletteDev& out0, long a_stride, long h_stride, int nchunks,
                                   const double* k255, bool hist, bool aligned, hipStream_t st);
+// Kcut and K3 over a batch (ds == 1): entries = (image, group) pairs needing a
+// cutoff search; B records (rules at rules0, slot offsets at off0) every
+// b_stride bytes; palette sums at out0 every c_stride bytes.  h_imgs: the same
+// image pointers on the host (alignment check).
+hipError_t launch_cutoffs_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n, int height,
+                                int width, const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
+                                const double* k255, const int2* entries, int n_entries,
+                                const unsigned short* chunk_hist0, long h_stride, GroupRule* rules0,
+                                long b_stride, hipStream_t st);
+size_t palette_sums_b_lds(int tl, int max_slots);
+hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n,
+                                     int height, int width, const GridParams& gp, const FastCls& fc,
+                                     const ClassTables* tabs, const double* k255, const GroupRule* rules0,
+                                     const double* off0, long b_stride, const int* nslots_img, int max_slots,
+                                     double* out0, long c_stride, hipStream_t st);
 // K1 for downsample_rate > 1 (one image).
 hipError_t launch_hsv_ds(const uint8_t* img, int height, int width, int ds, const GridParams& gp,
                          const FastCls& fc, const ClassTables* tabs, const PaletteDev& out, int nchunks,

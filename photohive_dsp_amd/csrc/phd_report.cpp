@@ -35,6 +35,7 @@ struct Layout {
     size_t b_rules, b_search, b_off, b_bytes;               // uploaded before K3
     size_t chunk_bytes;                                      // device only
     size_t ptr_bytes;                                        // image pointer array (pinned -> device)
+    size_t e_entries, e_ns, e_bytes;                         // Kcut (image, group) list + slots per image
     size_t dev_total, pin_total;
     size_t A(int i) const { return (size_t)i * a_bytes; }
     size_t C(int n, int i) const { return (size_t)n * a_bytes + (size_t)i * c_bytes; }
@@ -42,6 +43,8 @@ struct Layout {
     size_t H(int n, int i) const { return (size_t)n * (a_bytes + c_bytes + b_bytes) + (size_t)i * chunk_bytes; }
     size_t P_dev(int n) const { return (size_t)n * (a_bytes + c_bytes + b_bytes + chunk_bytes); }
     size_t P_pin(int n) const { return (size_t)n * (a_bytes + c_bytes + b_bytes); }
+    size_t E_dev(int n) const { return P_dev(n) + ptr_bytes; }
+    size_t E_pin(int n) const { return P_pin(n) + ptr_bytes; }
 };
 
 Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolblocks) {
@@ -61,8 +64,11 @@ Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolbl
     L.b_bytes = L.b_off + al(sizeof(double) * tl);
     L.chunk_bytes = al(sizeof(unsigned short) * (size_t)nchunks * tl);
     L.ptr_bytes = al(sizeof(void*) * (size_t)n);
-    L.dev_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes + L.chunk_bytes) + L.ptr_bytes;
-    L.pin_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes) + L.ptr_bytes;
+    L.e_entries = 0;
+    L.e_ns = al(2 * sizeof(int) * (size_t)n * tl);
+    L.e_bytes = L.e_ns + al(sizeof(int) * (size_t)n);
+    L.dev_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes + L.chunk_bytes) + L.ptr_bytes + L.e_bytes;
+    L.pin_total = (size_t)n * (L.a_bytes + L.c_bytes + L.b_bytes) + L.ptr_bytes + L.e_bytes;
     return L;
 }
 
@@ -338,34 +344,67 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipEventSynchronize(c->ev[5]));
     std::vector<PaletteDecision> dec(n);
     std::vector<int> ok(n, 1);
+    int* h_ent = (int*)(hp + L.E_pin(n) + L.e_entries);
+    int* h_ns = (int*)(hp + L.E_pin(n) + L.e_ns);
+    int n_ent = 0, max_slots = 1;
     for (int i = 0; i < n; i++) {
         const unsigned* hist = (const unsigned*)(hp + L.A(i) + L.a_hist);
+        uint8_t* b = hp + (size_t)n * (L.a_bytes + L.c_bytes) + (size_t)i * L.b_bytes;
+        h_ns[i] = 0;
         if (!decide_palette(gp, gc, hist, n_hsv, cfg, &dec[i])) {
             ok[i] = 0;
+            GroupRule* r = (GroupRule*)(b + L.b_rules);     // no slot: pass 2 keeps nothing
+            for (int g = 0; g < gp.tl; g++) r[g] = GroupRule{-1, 0, 0, 0, 0xFFFFFFFFu, 0u};
             continue;
         }
-        uint8_t* b = hp + (size_t)n * (L.a_bytes + L.c_bytes) + (size_t)i * L.b_bytes;
         memcpy(b + L.b_rules, dec[i].rules.data(), sizeof(GroupRule) * gp.tl);
         memcpy(b + L.b_search, dec[i].search.data(), sizeof(int) * dec[i].search.size());
         memcpy(b + L.b_off, dec[i].off.data(), sizeof(double) * dec[i].off.size());
+        for (int g : dec[i].search) {
+            h_ent[2 * n_ent] = i;
+            h_ent[2 * n_ent + 1] = g;
+            n_ent++;
+        }
+        h_ns[i] = (int)dec[i].parents.size();
+        max_slots = std::max(max_slots, h_ns[i]);
     }
     uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
     PHD_HIP(hipMemcpyAsync(dw + L.B(n, 0), hb, (size_t)n * L.b_bytes, hipMemcpyHostToDevice, st));
-    for (int i = 0; i < n; i++) {
-        if (!ok[i]) continue;
-        GroupRule* rules = (GroupRule*)(dw + L.B(n, i) + L.b_rules);
-        const int* search = (const int*)(dw + L.B(n, i) + L.b_search);
-        const double* off = (const double*)(dw + L.B(n, i) + L.b_off);
-        int ps = dec[i].search.empty() ? -1 : c->prof.begin(kCutoffs, st);
-        PHD_HIP(launch_palette_cutoffs(d_imgs[i], height, width, ds, gp,
-                                       (const unsigned short*)(dw + L.H(n, i)), nchunks, rules, search,
-                                       (int)dec[i].search.size(), c->d_k255, st));
+    const bool batched = ds <= 1 && palette_sums_b_lds(gp.tl, max_slots) <= 160 * 1024;
+    if (batched) {
+        // one Kcut and one K3 launch over the whole batch
+        PHD_HIP(hipMemcpyAsync(dw + L.E_dev(n), hp + L.E_pin(n), L.e_bytes, hipMemcpyHostToDevice, st));
+        const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(n));
+        int ps = n_ent ? c->prof.begin(kCutoffs, st) : -1;
+        PHD_HIP(launch_cutoffs_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
+                                     (const int2*)(dw + L.E_dev(n) + L.e_entries), n_ent,
+                                     (const unsigned short*)(dw + L.H(n, 0)), (long)L.chunk_bytes,
+                                     (GroupRule*)(dw + L.B(n, 0) + L.b_rules), (long)L.b_bytes, st));
         c->prof.end(ps, st);
         ps = c->prof.begin(kPalSums, st);
-        PHD_HIP(launch_palette_sums(d_imgs[i], height, width, ds, gp, rules, off,
-                                    (int)dec[i].parents.size(), (double*)(dw + L.C(n, i) + L.c_pal),
-                                    c->d_k255, st));
+        PHD_HIP(launch_palette_sums_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
+                                          (const GroupRule*)(dw + L.B(n, 0) + L.b_rules),
+                                          (const double*)(dw + L.B(n, 0) + L.b_off), (long)L.b_bytes,
+                                          (const int*)(dw + L.E_dev(n) + L.e_ns), max_slots,
+                                          (double*)(dw + L.C(n, 0) + L.c_pal), (long)L.c_bytes, st));
         c->prof.end(ps, st);
+    } else {
+        for (int i = 0; i < n; i++) {
+            if (!ok[i]) continue;
+            GroupRule* rules = (GroupRule*)(dw + L.B(n, i) + L.b_rules);
+            const int* search = (const int*)(dw + L.B(n, i) + L.b_search);
+            const double* off = (const double*)(dw + L.B(n, i) + L.b_off);
+            int ps = dec[i].search.empty() ? -1 : c->prof.begin(kCutoffs, st);
+            PHD_HIP(launch_palette_cutoffs(d_imgs[i], height, width, ds, gp,
+                                           (const unsigned short*)(dw + L.H(n, i)), nchunks, rules, search,
+                                           (int)dec[i].search.size(), c->d_k255, st));
+            c->prof.end(ps, st);
+            ps = c->prof.begin(kPalSums, st);
+            PHD_HIP(launch_palette_sums(d_imgs[i], height, width, ds, gp, rules, off,
+                                        (int)dec[i].parents.size(), (double*)(dw + L.C(n, i) + L.c_pal),
+                                        c->d_k255, st));
+            c->prof.end(ps, st);
+        }
     }
     PHD_HIP(hipEventRecord(c->ev[3], st));
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
@@ -446,11 +485,33 @@ bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, 
     memcpy(b + L.b_off, dec->off.data(), sizeof(double) * dec->off.size());
     PHD_HIP(hipMemcpyAsync(dw + L.B(1, 0), b, L.b_bytes, hipMemcpyHostToDevice, st));
     GroupRule* rules = (GroupRule*)(dw + L.B(1, 0) + L.b_rules);
-    PHD_HIP(launch_palette_cutoffs(d_img, height, width, ds, gp, pd.chunk_hist, nchunks, rules,
-                                   (const int*)(dw + L.B(1, 0) + L.b_search), (int)dec->search.size(),
-                                   c->d_k255, st));
-    PHD_HIP(launch_palette_sums(d_img, height, width, ds, gp, rules, (const double*)(dw + L.B(1, 0) + L.b_off),
-                                (int)dec->parents.size(), (double*)(dw + L.C(1, 0) + L.c_pal), c->d_k255, st));
+    const int np_ = (int)dec->parents.size();
+    if (ds <= 1 && palette_sums_b_lds(gp.tl, np_) <= 160 * 1024) {
+        // the production (batched) kernels, with a batch of one
+        int* h_ent = (int*)(hp + L.E_pin(1) + L.e_entries);
+        int* h_ns = (int*)(hp + L.E_pin(1) + L.e_ns);
+        const int n_ent = (int)dec->search.size();
+        for (int k = 0; k < n_ent; k++) {
+            h_ent[2 * k] = 0;
+            h_ent[2 * k + 1] = dec->search[k];
+        }
+        h_ns[0] = np_;
+        PHD_HIP(hipMemcpyAsync(dw + L.E_dev(1), hp + L.E_pin(1), L.e_bytes, hipMemcpyHostToDevice, st));
+        const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(1));
+        PHD_HIP(launch_cutoffs_batch(d_ptrs, &d_img, 1, height, width, gp, cls->fc, cls->d, c->d_k255,
+                                     (const int2*)(dw + L.E_dev(1) + L.e_entries), n_ent, pd.chunk_hist,
+                                     (long)L.chunk_bytes, rules, (long)L.b_bytes, st));
+        PHD_HIP(launch_palette_sums_batch(d_ptrs, &d_img, 1, height, width, gp, cls->fc, cls->d, c->d_k255,
+                                          rules, (const double*)(dw + L.B(1, 0) + L.b_off), (long)L.b_bytes,
+                                          (const int*)(dw + L.E_dev(1) + L.e_ns), np_,
+                                          (double*)(dw + L.C(1, 0) + L.c_pal), (long)L.c_bytes, st));
+    } else {
+        PHD_HIP(launch_palette_cutoffs(d_img, height, width, ds, gp, pd.chunk_hist, nchunks, rules,
+                                       (const int*)(dw + L.B(1, 0) + L.b_search), (int)dec->search.size(),
+                                       c->d_k255, st));
+        PHD_HIP(launch_palette_sums(d_img, height, width, ds, gp, rules, (const double*)(dw + L.B(1, 0) + L.b_off),
+                                    np_, (double*)(dw + L.C(1, 0) + L.c_pal), c->d_k255, st));
+    }
     const int np = (int)dec->parents.size();
     std::vector<double> pal(4 * np);
     PHD_HIP(hipMemcpyAsync(pal.data(), dw + L.C(1, 0) + L.c_pal, sizeof(double) * 4 * np,
