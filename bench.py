@@ -142,16 +142,10 @@ def main():
     elapsed = time.perf_counter() - t0
     kern = kernel_times()
 
-    # the single collective: [elapsed (max), images, pixels] -> merged counters
-    counters = torch.tensor([elapsed, float(B * args.steps), float(B * args.steps * H * W)],
-                            dtype=torch.float64, device="cuda")
-    if world > 1:
-        import torch.distributed as dist
-        mx = counters[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        counters[0] = mx[0]
-    elapsed, images = float(counters[0]), float(counters[1])
+    # the single collective: max of wall time, sums of images / pixels (shard.py)
+    from photohive_dsp_amd.shard import merge_counters
+    elapsed, images, _ = merge_counters(elapsed, float(B * args.steps), float(B * args.steps * H * W),
+                                        device="cuda")
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()

@@ -1,0 +1,63 @@
+"""Multi-GPU sharding of independent images.
+
+Images are independent and each fits one GPU, so the batch is partitioned
+across ranks with no data-path collective: every rank reports on its own
+images and keeps its results.  The only collective merges a few counters
+(images, pixels, wall time) -- a sum for counts and a max for time -- over
+RCCL (backend "nccl") on the GPU box or gloo in the CPU tests.
+
+Mixed sizes (BASELINE.json config 5) are balanced with a static LPT
+assignment: images sorted by pixel count, largest first, each onto the
+least-loaded rank (ties: lower rank, then lower index -- deterministic, so
+every rank computes the same plan without communicating).
+"""
+from __future__ import annotations
+
+import heapq
+from typing import List, Sequence, Tuple
+
+# config 5's size list (2*3*5-smooth shapes, aspect within 1:5..5:1), SURVEY.md 8d
+MIXED_SHAPES = [(512, 512), (480, 640), (720, 1280), (1080, 1920), (1536, 2048), (2000, 3000),
+                (3000, 4000), (4000, 6000), (640, 480), (1280, 720), (3000, 2000), (6000, 4000)]
+
+
+def mixed_sizes(n: int, seed: int) -> List[Tuple[int, int]]:
+    """n (H, W) shapes drawn by seed from MIXED_SHAPES (splitmix64, as synth)."""
+    from .synth import splitmix64
+    words = splitmix64(seed, n)
+    return [MIXED_SHAPES[int(w % len(MIXED_SHAPES))] for w in words]
+
+
+def assign(sizes: Sequence[Tuple[int, int]], world: int) -> List[List[int]]:
+    """LPT partition of image indices over `world` ranks by pixel count.
+    Returns per-rank index lists, each in ascending image order."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    order = sorted(range(len(sizes)), key=lambda i: (-sizes[i][0] * sizes[i][1], i))
+    heap = [(0, r) for r in range(world)]
+    out: List[List[int]] = [[] for _ in range(world)]
+    for i in order:
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + sizes[i][0] * sizes[i][1], r))
+    return [sorted(x) for x in out]
+
+
+def loads(sizes: Sequence[Tuple[int, int]], plan: List[List[int]]) -> List[int]:
+    """Pixels per rank of a plan."""
+    return [sum(sizes[i][0] * sizes[i][1] for i in idx) for idx in plan]
+
+
+def merge_counters(elapsed_s: float, images: float, pixels: float, device=None):
+    """The single collective: max of wall time, sum of images and pixels over
+    the default process group (identity when torch.distributed is not
+    initialised).  Returns (elapsed_max, images_total, pixels_total)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed_s, images, pixels], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        mx = t[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t[0] = mx[0]
+    return float(t[0]), float(t[1]), float(t[2])
