@@ -186,6 +186,12 @@ int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, const phd_c
 int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int height, int width, const phd_config* cfg,
                           int ablate, int iters, double* avg_ms);
 
+/* Validation hook: the power spectrum |X[u][k]|^2 (src/fft_processing.c:48-50)
+ * of one device RGB8 image through the production FFT kernels, column-major
+ * into d_out[(width/2+1) * height] (device memory).  0, -2 when the size has
+ * no compile-time FFT plan, or -1. */
+int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int width, double* d_out);
+
 /* Free an Image_PGM returned by get_blur_profile_visual. */
 void phd_free_pgm(Image_PGM* img);
 

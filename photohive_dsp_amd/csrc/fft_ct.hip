@@ -1,0 +1,362 @@
+// fft_ct.hip -- the 2-D power spectrum and polar binning for image sizes with a
+// compile-time FFT plan (fft_engine.h; the plan lists are PHD_CT_ROWS /
+// PHD_CT_COLS in phd_internal.h).  Other sizes take fft.hip's runtime-plan
+// kernels.
+//
+// Replaces rgb2pgm + remove_dc_bias (src/image_processing.c:505-512,
+// src/blur_profile.c:233-238), pgm_fft (src/fft_processing.c:18-63: FFTW r2c,
+// unnormalised, e^{-i}), pgm_normalize_fft (:173-213) and the binning loop of
+// calculate_blur_profile (src/blur_profile.c:87-100).
+//
+// Row kernel (persistent, 2 blocks per CU).  Each step handles one pair of
+// image rows.  Both rows' RGB8 bytes were prefetched into registers (dwordx3 =
+// 4 pixels) during the previous step.  They become luma - avg and are packed
+// as one complex row (row y0 real, row y0+1 imaginary) in LDS.  The next pair's
+// loads are issued, then the FFT runs in LDS.  The two half spectra are
+// separated, A[k] = (Z[k] + conj Z[W-k]) / 2 and B[k] = (Z[k] - conj Z[W-k]) / 2i,
+// and stored column-major into inter[k][H].  The 4 pairs that share a 128-byte
+// line of every column run at the same time on one XCD, so the 32-byte pieces
+// merge in that XCD's L2.
+//
+// Column kernel (persistent, 2 blocks per CU, a contiguous range of columns
+// per block).  The next column is prefetched into registers.  The last pass's
+// outputs never go back to LDS: the epilogue forms p = re^2 + im^2, keeps the
+// block's max and sums log(p) for p >= 1 into the element's polar bin.  Lanes
+// hold consecutive spectrum rows, so a wave covers few bins: one masked wave
+// sum and one LDS atomic per distinct bin.  The block adds its non-zero bins
+// to the image's bin sums at the end.
+//
+// log(p) for the bins: p = m * 2^e (frexp), log p = e ln2 + log(m) with log(m)
+// in fp32.  The absolute error is <= 2e-7 per element, against bin averages of
+// order 10 (north_star tolerance: 1e-4 relative).  The max and the p >= 1 test
+// stay in fp64.
+#include <cstdlib>
+
+// Nothing in this file needs the reference's rounding (the FFT only has to be
+// within the north_star tolerance), so fused multiply-adds are allowed here.
+#pragma clang fp contract(fast)
+
+#include "fft_engine.h"
+#include "phd_device.h"
+
+namespace phd {
+
+namespace {
+
+using namespace fe;
+
+__device__ __forceinline__ double2 sel4(int e, double2 a, double2 b, double2 c, double2 d) {
+    return e == 0 ? a : (e == 1 ? b : (e == 2 ? c : d));
+}
+
+constexpr double kWr = 0.299 / 255.0, kWg = 0.587 / 255.0, kWb = 0.114 / 255.0;
+
+__device__ __forceinline__ int byte_of(const unsigned (&w)[3], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255; }
+
+template <int W, int T, int... Rs>
+struct RowK {
+    static constexpr int NTW = tw_entries<1, Rs...>();
+    static constexpr int G4 = W / 4;                       // 4-pixel groups per row
+    static constexpr int LR = (G4 + T - 1) / T;            // groups per thread
+    static constexpr size_t lds = sizeof(double2) * (W + NTW);
+    static_assert(W % 4 == 0, "row plans need W % 4 == 0");
+    static_assert(Radices<Rs...>::product == W, "plan");
+};
+
+template <int W, int T, int... Rs>
+__global__ __launch_bounds__(T) void k_rows_ct(const uint8_t* __restrict__ img, int H,
+                                               const unsigned long long* __restrict__ sums,
+                                               const double* __restrict__ k255g, const double2* __restrict__ twg,
+                                               double2* __restrict__ inter) {
+    using K = RowK<W, T, Rs...>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double2* buf = reinterpret_cast<double2*>(smem);
+    double2* tw = buf + W;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
+    // avg = (Br + Bg + Bb) / 3 (src/interface.c:78) from the exact channel sums
+    const double n = (double)H * (double)W;
+    const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
+                        (double)sums[2] / 255.0 / n) / 3.0;
+    // schedule: line group m (pairs 4m..4m+3) on XCD m % 8, its 4 pairs on 4
+    // blocks of that XCD (gridDim.x is a multiple of 32)
+    const int P = (H + 1) / 2;
+    const int x = blockIdx.x & 7, q = blockIdx.x >> 3, QA = gridDim.x >> 5;
+    const int a = q >> 2, i4 = q & 3;
+    auto pair_of = [&](int s) { return 4 * (x + 8 * (a + s * QA)) + i4; };
+
+    unsigned rg[K::LR][2][3];
+    auto fetch = [&](int pr) {
+        const int y0 = 2 * pr;
+        const unsigned* r0 = reinterpret_cast<const unsigned*>(img + (size_t)y0 * 3 * W);
+        const unsigned* r1 = (y0 + 1 < H) ? r0 + 3 * W / 4 : r0;
+#pragma unroll
+        for (int j = 0; j < K::LR; j++) {
+            const int g = tid + j * T;
+            if (K::G4 % T == 0 || g < K::G4) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    rg[j][0][c] = __builtin_nontemporal_load(r0 + 3 * g + c);
+                    rg[j][1][c] = __builtin_nontemporal_load(r1 + 3 * g + c);
+                }
+            }
+        }
+    };
+    int s = 0, pr = pair_of(0);
+    if (pr < P) fetch(pr);
+    __syncthreads();
+    const int rot = (tid >> 1) & 3;   // b128 write swizzle: 8 lanes of a group hit 8 distinct 16-B slots
+    while (pr < P) {
+        const int y0 = 2 * pr;
+        const bool two = y0 + 1 < H;
+#pragma unroll
+        for (int j = 0; j < K::LR; j++) {
+            const int g = tid + j * T;
+            if (K::G4 % T == 0 || g < K::G4) {
+                double2 z[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    // rgb2pgm (src/image_processing.c:509) with k/255 folded into the
+                    // weights (within 2 ulp), remove_dc_bias (src/blur_profile.c:236)
+                    const double p0 = kWr * byte_of(rg[j][0], 3 * e) + kWg * byte_of(rg[j][0], 3 * e + 1) +
+                                      kWb * byte_of(rg[j][0], 3 * e + 2);
+                    const double p1 = kWr * byte_of(rg[j][1], 3 * e) + kWg * byte_of(rg[j][1], 3 * e + 1) +
+                                      kWb * byte_of(rg[j][1], 3 * e + 2);
+                    z[e] = make_double2(p0 - avg, two ? p1 - avg : 0.0);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int ee = (e + rot) & 3;
+                    buf[4 * g + ee] = sel4(ee, z[0], z[1], z[2], z[3]);
+                }
+            }
+        }
+        const int prn = pair_of(s + 1);
+        if (prn < P) fetch(prn);
+        __syncthreads();
+        fft_lds<W, T, 1, Rs...>(buf, tw, tid);
+        constexpr int WF = W / 2 + 1;
+        for (int k = tid; k < WF; k += T) {
+            const double2 zk = buf[k], zm = buf[k == 0 ? 0 : W - k];
+            double2* o = inter + (size_t)k * H + y0;
+            o[0] = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+            if (two) o[1] = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+        }
+        __syncthreads();
+        s++;
+        pr = prn;
+    }
+}
+
+// log(p) for p >= 1: e ln2 + log(m) with m = frexp mantissa and log(m) in fp32
+__device__ __forceinline__ double log_p(double p) {
+    int e;
+    const double m = frexp(p, &e);
+    return (double)e * 0.69314718055994530942 + (double)__logf((float)m);
+}
+
+template <int H, int T, int... Rs>
+struct ColK {
+    using PL = Plan<H, T, 1, Rs...>;
+    using L = typename PL::Last;
+    static constexpr int R = Radices<Rs...>::count > 0 ? H / L::NB : 1;   // last radix
+    static constexpr int NTW = tw_entries<1, Rs...>();
+    static constexpr int CR = (H + T - 1) / T;                            // prefetch rounds
+    static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
+    static size_t lds(int nbins) { return sizeof(double2) * (H + NTW) + sizeof(double) * nbins; }
+    static_assert(Radices<Rs...>::product == H, "plan");
+};
+
+template <int H, int T, int... Rs>
+__global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter, int wf,
+                                               const uint16_t* __restrict__ binmap, int nbins,
+                                               double* __restrict__ bin_sums, double* __restrict__ fmax_part,
+                                               const double2* __restrict__ twg, double* __restrict__ dbg) {
+    using K = ColK<H, T, Rs...>;
+    using L = typename K::L;
+    constexpr int R = K::R;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double2* buf = reinterpret_cast<double2*>(smem);
+    double2* tw = buf + H;
+    double* lb = reinterpret_cast<double*>(tw + K::NTW);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
+    for (int i = tid; i < nbins; i += T) lb[i] = 0.0;
+    const int c0 = (int)((long)blockIdx.x * wf / gridDim.x), c1 = (int)((long)(blockIdx.x + 1) * wf / gridDim.x);
+    double2 pf[K::CR];
+    auto fetch = [&](int col) {
+        const double2* src = inter + (size_t)col * H;
+#pragma unroll
+        for (int c = 0; c < K::CR; c++) {
+            const int i = tid + c * T;
+            if (H % T == 0 || i < H) pf[c] = src[i];
+        }
+    };
+    if (c0 < c1) fetch(c0);
+    double mx = 0.0;
+    __syncthreads();
+    for (int col = c0; col < c1; col++) {
+#pragma unroll
+        for (int c = 0; c < K::CR; c++) {
+            const int i = tid + c * T;
+            if (H % T == 0 || i < H) buf[i] = pf[c];
+        }
+        // bin ids of this thread's run of the column: u in [tid*E, tid*E + E)
+        uint16_t bm[K::E];
+        const uint16_t* bcol = binmap + (size_t)col * H + tid * K::E;
+#pragma unroll
+        for (int j = 0; j < K::E; j++) bm[j] = (H % K::E == 0 && K::E * T == H) || tid * K::E + j < H ? bcol[j] : 0;
+        if (col + 1 < c1) fetch(col + 1);
+        __syncthreads();
+        K::PL::all_but_last(buf, tw, tid);
+        double2 v[L::ROUNDS][R];
+        L::load(buf, v, tid);
+        L::compute(v, tw + K::PL::last_tw_offset, tid);
+        __syncthreads();                       // every thread has read its last-pass inputs
+        double* lgb = reinterpret_cast<double*>(buf);   // log p per spectrum row, -1 for p < 1
+#pragma unroll
+        for (int q = 0; q < L::ROUNDS; q++) {
+            const int b = tid + q * T;
+            if (L::active(b)) {
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    const double2 X = v[q][k];
+                    const double p = X.x * X.x + X.y * X.y;          // src/fft_processing.c:49
+                    mx = fmax(mx, p);
+                    if (dbg) dbg[(size_t)col * H + b + k * L::NB] = p;
+                    lgb[b + k * L::NB] = p >= 1 ? log_p(p) : -1.0;   // src/fft_processing.c:197-198
+                }
+            }
+        }
+        __syncthreads();
+        // contiguous runs of one bin: one LDS atomic per run (bins change every
+        // few tens of rows along a column)
+        {
+            int cur = -1;
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < K::E; j++) {
+                const int u = tid * K::E + j;
+                if ((H % K::E == 0 && K::E * T == H) || u < H) {
+                    const double lg = lgb[u];
+                    if (lg >= 0.0) {
+                        const int bin = bm[j];
+                        if (bin != cur) {
+                            if (cur >= 0) atomicAdd(&lb[cur], acc);
+                            cur = bin;
+                            acc = 0.0;
+                        }
+                        acc += lg;
+                    }
+                }
+            }
+            if (cur >= 0) atomicAdd(&lb[cur], acc);
+        }
+        __syncthreads();
+    }
+    // block max -> one partial per block; non-zero bins -> the image's sums
+    mx = wave_max(mx);
+    double* red = reinterpret_cast<double*>(buf);
+    if (lane_id() == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        double m = 0.0;
+        for (int w = 0; w < T / 64; w++) m = fmax(m, red[w]);
+        fmax_part[blockIdx.x] = m;
+    }
+    for (int i = tid; i < nbins; i += T) {
+        const double t = lb[i];
+        if (t != 0.0) atomicAdd(&bin_sums[i], t);
+    }
+}
+
+template <typename K>
+void allow_big_lds(K kernel) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+
+int row_grid() {
+    const int g = (2 * num_cus()) / 32 * 32;
+    return g > 32 ? g : 32;
+}
+
+template <int W, int T, int... Rs>
+hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, const double* k255,
+                   const double2* tw, double2* inter, hipStream_t st) {
+    static bool once = (allow_big_lds(k_rows_ct<W, T, Rs...>), true);
+    (void)once;
+    const size_t lds = RowK<W, T, Rs...>::lds;
+    hipLaunchKernelGGL((k_rows_ct<W, T, Rs...>), dim3(row_grid()), dim3(T), lds, st, img, H, sums, k255, tw, inter);
+    return hipGetLastError();
+}
+
+template <int H, int T, int... Rs>
+hipError_t cols_ct(const double2* inter, int wf, const uint16_t* binmap, int nbins, double* bin_sums,
+                   double* fmax_part, const double2* tw, double* dbg, hipStream_t st) {
+    static bool once = (allow_big_lds(k_cols_ct<H, T, Rs...>), true);
+    (void)once;
+    const size_t lds = ColK<H, T, Rs...>::lds(nbins);
+    hipLaunchKernelGGL((k_cols_ct<H, T, Rs...>), dim3(fft_cols_ct_blocks(H, wf)), dim3(T), lds, st, inter, wf, binmap,
+                       nbins, bin_sums, fmax_part, tw, dbg);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool ct_rows_plan(int w, std::vector<int>* radices) {
+#define PHD_X(N, T, ...)                             \
+    if (w == N) {                                    \
+        if (radices) *radices = std::vector<int>{__VA_ARGS__}; \
+        return true;                                 \
+    }
+    PHD_CT_ROWS(PHD_X)
+#undef PHD_X
+    return false;
+}
+
+bool ct_cols_plan(int h, std::vector<int>* radices) {
+#define PHD_X(N, T, ...)                             \
+    if (h == N) {                                    \
+        if (radices) *radices = std::vector<int>{__VA_ARGS__}; \
+        return true;                                 \
+    }
+    PHD_CT_COLS(PHD_X)
+#undef PHD_X
+    return false;
+}
+
+size_t fft_cols_ct_lds(int h, int nbins) {
+#define PHD_X(N, T, ...) \
+    if (h == N) return ColK<N, T, __VA_ARGS__>::lds(nbins);
+    PHD_CT_COLS(PHD_X)
+#undef PHD_X
+    return 0;
+}
+
+int fft_cols_ct_blocks(int height, int wf) {
+    (void)height;
+    const int g = 2 * num_cus();
+    return wf < g ? wf : g;
+}
+
+hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
+                              const double* k255, const double2* tw, double2* inter, hipStream_t st) {
+#define PHD_X(N, T, ...) \
+    if (width == N) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, st);
+    PHD_CT_ROWS(PHD_X)
+#undef PHD_X
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_fft_cols_ct(const double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
+                              double* bin_sums, double* fmax_part, const double2* tw, double* dbg,
+                              hipStream_t st) {
+#define PHD_X(N, T, ...) \
+    if (height == N) return cols_ct<N, T, __VA_ARGS__>(inter, wf, binmap, nbins, bin_sums, fmax_part, tw, dbg, st);
+    PHD_CT_COLS(PHD_X)
+#undef PHD_X
+    return hipErrorInvalidValue;
+}
+
+}  // namespace phd

@@ -154,6 +154,75 @@ const FftPlanHost* get_plan(Context* c, int n) {
     return &(c->plans[n] = p);
 }
 
+const double2* get_ct_twiddles(Context* c, int n, bool rows) {
+    const auto key = std::make_pair(n, rows ? 1 : 0);
+    auto it = c->ct_tw.find(key);
+    if (it != c->ct_tw.end()) return it->second;
+    std::vector<int> rad;
+    if (!(rows ? ct_rows_plan(n, &rad) : ct_cols_plan(n, &rad))) {
+        set_error("no compile-time FFT plan for length " + std::to_string(n));
+        return nullptr;
+    }
+    // pass p (NS = R0 * ... * R(p-1) > 1): W_{NS*Rp}^jm for jm < NS
+    const long double two_pi = 6.283185307179586476925286766559005768L;
+    std::vector<double2> tw;
+    long ns = 1;
+    for (int r : rad) {
+        if (ns > 1)
+            for (long jm = 0; jm < ns; jm++) {
+                const long double a = two_pi * (long double)jm / (long double)(ns * r);
+                tw.push_back(make_double2((double)cosl(a), (double)-sinl(a)));
+            }
+        ns *= r;
+    }
+    if (tw.empty()) tw.push_back(make_double2(1.0, 0.0));
+    double2* d = nullptr;
+    if (hipMalloc(&d, sizeof(double2) * tw.size()) != hipSuccess ||
+        hipMemcpy(d, tw.data(), sizeof(double2) * tw.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("compile-time FFT twiddle upload failed");
+        return nullptr;
+    }
+    c->ct_tw[key] = d;
+    return d;
+}
+
+bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s) {
+    *s = FftSel{};
+    static const bool force_generic = getenv("PHD_FFT_GENERIC") != nullptr;   // A/B experiments only
+    bool ct = !force_generic && ct_rows_plan(width, nullptr) && ct_cols_plan(height, nullptr) &&
+              fft_cols_ct_lds(height, nbins) <= 160 * 1024;
+    for (int i = 0; ct && i < n; i++)
+        if (reinterpret_cast<uintptr_t>(imgs[i]) & 3) ct = false;   // dword row loads
+    if (ct) {
+        s->ct = true;
+        s->tw_r = get_ct_twiddles(c, width, true);
+        s->tw_c = get_ct_twiddles(c, height, false);
+        if (!s->tw_r || !s->tw_c) return false;
+        s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1);
+        return true;
+    }
+    s->prow = get_plan(c, width);
+    s->pcol = get_plan(c, height);
+    if (!s->prow || !s->pcol) return false;
+    const int wf = width / 2 + 1;
+    const int C = fft_cols_blocks(height, wf, nbins, s->pcol->plan, nullptr, nullptr);
+    s->col_blocks = (wf + C - 1) / C;
+    return true;
+}
+
+hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
+                           const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st) {
+    return s.ct ? launch_fft_rows_ct(img, height, width, sums, k255, s.tw_r, inter, st)
+                : launch_fft_rows(img, height, width, s.prow->plan, sums, k255, inter, st);
+}
+
+hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int wf, const uint16_t* binmap,
+                           int nbins, double* bin_sums, double* fmax_part, double* dbg, hipStream_t st) {
+    if (s.ct) return launch_fft_cols_ct(inter, height, wf, binmap, nbins, bin_sums, fmax_part, s.tw_c, dbg, st);
+    if (dbg) return hipErrorNotSupported;
+    return launch_fft_cols(inter, height, wf, s.pcol->plan, binmap, nbins, bin_sums, fmax_part, st);
+}
+
 const BlurTable* get_table(Context* c, int height, int width, int nr, int na) {
     auto key = std::make_tuple(height, width, nr, na);
     auto it = c->tables.find(key);

@@ -92,6 +92,7 @@ struct Context {
     hipStream_t stream = nullptr;
     double* d_k255 = nullptr;                       // k/255.0 for k in [0,256)
     std::map<int, FftPlanHost> plans;
+    std::map<std::pair<int, int>, double2*> ct_tw;  // (length, rows?) -> compile-time plan twiddles
     std::map<std::tuple<int, int, int, int>, BlurTable> tables;
     struct Cls {
         FastCls fc;
@@ -118,6 +119,24 @@ Context* get_context();
 bool ensure_device(void** p, size_t* cap, size_t need);
 bool ensure_pinned(Context* c, size_t need);
 const FftPlanHost* get_plan(Context* c, int n);
+// Per-pass twiddle tables of the compile-time plan of length n (rows or columns).
+const double2* get_ct_twiddles(Context* c, int n, bool rows);
+
+// The FFT kernels one image size takes: the compile-time plans when both
+// lengths have one (fft_ct.hip), else the runtime-plan kernels (fft.hip).
+struct FftSel {
+    bool ct = false;
+    const FftPlanHost* prow = nullptr;
+    const FftPlanHost* pcol = nullptr;
+    const double2* tw_r = nullptr;
+    const double2* tw_c = nullptr;
+    int col_blocks = 0;   // entries of the per-block max partials
+};
+bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s);
+hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
+                           const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st);
+hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int wf, const uint16_t* binmap,
+                           int nbins, double* bin_sums, double* fmax_part, double* dbg, hipStream_t st);
 const BlurTable* get_table(Context* c, int height, int width, int nr, int na);
 // Classification tables of a grid (uploaded once per configuration).
 const Context::Cls* get_cls(Context* c, const GridParams& gp);

@@ -6,6 +6,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace phd {
 
 // Pixels per palette chunk: the unit of work of the hsv/stats kernel and the
@@ -128,6 +130,24 @@ hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPl
                            double* fmax_part, hipStream_t st);
 // Column blocks of launch_fft_cols (= entries of fmax_part); optional LDS size.
 int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds, int* lds_bins);
+
+// ---- compile-time FFT plans (fft_ct.hip / fft_engine.h) ------------------------
+// X(length, threads per block, radices...).  The first radix is odd (LDS
+// bank-conflict-free first pass, fft_engine.h).  Rows need length % 4 == 0.
+#define PHD_CT_ROWS(X) X(4000, 256, 25, 16, 10)
+#define PHD_CT_COLS(X) X(3000, 256, 15, 20, 10)
+// radices of the compile-time plan for a row / column length (false: none)
+bool ct_rows_plan(int w, std::vector<int>* radices);
+bool ct_cols_plan(int h, std::vector<int>* radices);
+size_t fft_cols_ct_lds(int height, int nbins);
+int fft_cols_ct_blocks(int height, int wf);
+// tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built)
+hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
+                              const double* k255, const double2* tw, double2* inter, hipStream_t st);
+// dbg (optional): the power spectrum, column-major [wf][height]
+hipError_t launch_fft_cols_ct(const double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
+                              double* bin_sums, double* fmax_part, const double2* tw, double* dbg,
+                              hipStream_t st);
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st);
 hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st);

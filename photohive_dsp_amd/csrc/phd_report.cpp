@@ -289,14 +289,13 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const int nbins = cfg.radius_partitions * cfg.angle_partitions;
     const int ncrops = crops ? crops->N : 0;
     const int wf = width / 2 + 1;
-    const FftPlanHost* prow = get_plan(c, width);
-    const FftPlanHost* pcol = get_plan(c, height);
+    FftSel fs;
+    if (!select_fft(c, height, width, nbins, d_imgs, n, &fs)) return false;
     const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
     const Context::Cls* cls = get_cls(c, gp);
-    if (!prow || !pcol || !tbl || !cls) return false;
+    if (!tbl || !cls) return false;
 
-    const int C = fft_cols_blocks(height, wf, nbins, pcol->plan, nullptr, nullptr);
-    const int ncolblocks = (wf + C - 1) / C;
+    const int ncolblocks = fs.col_blocks;
     const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, sizeof(double2) * (size_t)height * wf))
@@ -325,10 +324,10 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
         double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
         int ps = c->prof.begin(kFftRows, st);
-        PHD_HIP(launch_fft_rows(d_imgs[i], height, width, prow->plan, sums, c->d_k255, c->d_inter, st));
+        PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255, c->d_inter, st));
         c->prof.end(ps, st);
         ps = c->prof.begin(kFftCols, st);
-        PHD_HIP(launch_fft_cols(c->d_inter, height, wf, pcol->plan, tbl->d_map, nbins, bins, fmx, st));
+        PHD_HIP(launch_cols_sel(fs, c->d_inter, height, wf, tbl->d_map, nbins, bins, fmx, nullptr, st));
         c->prof.end(ps, st);
         if (ncrops) {
             // crop boxes: sharpness on the full-resolution luma before DC removal
@@ -850,10 +849,10 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
     const int nchunks = (int)((n_hsv + kChunk - 1) / kChunk);
     const Context::Cls* cls = get_cls(c, gp);
     const int wf = width / 2 + 1;
-    const FftPlanHost* prow = get_plan(c, width);
-    const FftPlanHost* pcol = get_plan(c, height);
     const BlurTable* tbl = get_table(c, height, width, cfg->radius_partitions, cfg->angle_partitions);
-    if (!cls || !prow || !pcol || !tbl) return -1;
+    FftSel fs;
+    if (!cls || !tbl || !select_fft(c, height, width, cfg->radius_partitions * cfg->angle_partitions, &d_rgb, 1, &fs))
+        return -1;
     // scratch outputs in the (large enough) workspace of the report just run
     uint8_t* dw = (uint8_t*)c->d_ws;
     PaletteDev pd;
@@ -878,10 +877,10 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
                            : launch_hsv_stats_batch(d_ptr, 1, height, width, gp, cls->fc, cls->d, pd, 0, 0, nchunks,
                                                     c->d_k255, kernel == kK1, all_aligned(&d_rgb, 1), st);
                 break;
-            case kFftRows: e = launch_fft_rows(d_rgb, height, width, prow->plan, pd.sums, c->d_k255, c->d_inter, st); break;
-            case kFftCols: e = launch_fft_cols(c->d_inter, height, wf, pcol->plan, tbl->d_map,
+            case kFftRows: e = launch_rows_sel(fs, d_rgb, height, width, pd.sums, c->d_k255, c->d_inter, st); break;
+            case kFftCols: e = launch_cols_sel(fs, c->d_inter, height, wf, tbl->d_map,
                                                cfg->radius_partitions * cfg->angle_partitions, (double*)pd.chunk_hist,
-                                               (double*)pd.chunk_hist + 65536, st); break;
+                                               (double*)pd.chunk_hist + 65536, nullptr, st); break;
             default: set_error("kernel not supported by the timing hook"); g_ablate = 0; return -1;
         }
         if (e != hipSuccess) {
@@ -896,5 +895,50 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
     float ms = 0;
     (void)hipEventElapsedTime(&ms, a, b);
     *avg_ms = ms / iters;
+    return 0;
+}
+
+// Validation hook: the power spectrum |X[u][k]|^2 of one device image through
+// the production FFT kernels (compile-time plans only), column-major into
+// d_out[(W/2+1) * H] (device).  Returns 0, -2 when the size has no
+// compile-time plan, or -1.
+extern "C" int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int width, double* d_out) {
+    clear_error();
+    Context* c = get_context();
+    if (!c || !d_out) return -1;
+    phd_config cfg;
+    phd_config_default(&cfg);
+    {
+        Full_Report_Data* r = nullptr;
+        int st = -1;
+        std::lock_guard<std::mutex> lk(c->mu);
+        const uint8_t* imgs[1] = {d_rgb};
+        if (!run_reports(c, imgs, 1, height, width, cfg, nullptr, &r, &st, nullptr)) return -1;
+        free_full_report(&r);
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int nbins = cfg.radius_partitions * cfg.angle_partitions;
+    const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
+    FftSel fs;
+    if (!tbl || !select_fft(c, height, width, nbins, &d_rgb, 1, &fs)) return -1;
+    if (!fs.ct) {
+        set_error("no compile-time FFT plan for this size");
+        return -2;
+    }
+    // the report just run left the image's channel sums at the start of the workspace
+    uint8_t* dw = (uint8_t*)c->d_ws;
+    const int wf = width / 2 + 1;
+    double* scratch = nullptr;
+    if (hipMalloc(&scratch, sizeof(double) * (nbins + 4096)) != hipSuccess) return -1;
+    const hipStream_t st = c->stream;
+    hipError_t e = launch_rows_sel(fs, d_rgb, height, width, (const unsigned long long*)dw, c->d_k255, c->d_inter, st);
+    if (e == hipSuccess)
+        e = launch_cols_sel(fs, c->d_inter, height, wf, tbl->d_map, nbins, scratch, scratch + nbins, d_out, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(scratch);
+    if (e != hipSuccess) {
+        set_error(std::string("power spectrum hook: ") + hipGetErrorString(e));
+        return -1;
+    }
     return 0;
 }

@@ -79,6 +79,8 @@ KERNELS = ["hsv_stats", "fft_rows", "fft_cols", "palette_cutoffs", "palette_sums
 lib.phd_debug_time_kernel.restype = ctypes.c_int
 lib.phd_debug_time_kernel.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(PhdConfig),
                                       ctypes.c_int, ctypes.c_int, P(ctypes.c_double)]
+lib.phd_debug_power_spectrum.restype = ctypes.c_int
+lib.phd_debug_power_spectrum.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 lib.free_full_report.restype = None
 lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
 lib.phd_free_pgm.argtypes = [P(Image_PGM)]

@@ -34,6 +34,13 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_every_declared_function_has_ctypes_argtypes():
+    """A pointer passed without argtypes is truncated to a C int by ctypes."""
+    from photohive_dsp_amd.lib import lib
+    missing = [f for f in declared_functions() if getattr(lib, f).argtypes is None and f != "phd_last_error"]
+    assert not missing, missing
+
+
 def test_struct_layouts_match_reference_binding():
     from photohive_dsp_amd import structures as S
     # x86-64 sizes of the reference structs (src/*.h)

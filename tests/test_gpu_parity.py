@@ -253,3 +253,34 @@ def test_hsv_group_exhaustive_rgb_cube(cfg):
     assert bad.size == 0, f"{bad.size} hsv mismatches, e.g. rgb={cube[bad[:5]].tolist()} " \
                           f"gpu={got_hsv[bad[:3]].tolist()} cpu={want_hsv[bad[:3]].tolist()}"
     np.testing.assert_array_equal(d_gid.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("kind,seed", [("uniform", 5), ("structured", 6)])
+def test_power_spectrum_compile_time_fft_4000x3000(kind, seed):
+    """The production FFT kernels' |X|^2 against numpy's rfft2 (pocketfft, fp64)
+    of the reference's luma - DC bias (src/image_processing.c:505-512,
+    src/blur_profile.c:233-238, src/fft_processing.c:34-50)."""
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    H, W = 3000, 4000
+    img = synth.make(kind, H, W, seed)
+    t = torch.from_numpy(np.ascontiguousarray(img)).cuda()
+    wf = W // 2 + 1
+    out = torch.empty(wf * H, dtype=torch.float64, device="cuda")
+    rc = L.lib.phd_debug_power_spectrum(t.data_ptr(), H, W, out.data_ptr())
+    if rc == -2:
+        pytest.skip("no compile-time FFT plan for this size")
+    assert rc == 0, L.last_error()
+    got = out.cpu().numpy().reshape(wf, H).T
+    k255 = np.arange(256, dtype=np.float64) / 255.0
+    f = img.astype(np.int64)
+    pgm = 0.299 * k255[f[..., 0]] + 0.587 * k255[f[..., 1]] + 0.114 * k255[f[..., 2]]
+    n = float(H * W)
+    avg = (f[..., 0].sum() / 255.0 / n + f[..., 1].sum() / 255.0 / n + f[..., 2].sum() / 255.0 / n) / 3.0
+    X = np.fft.rfft2(pgm - avg)
+    want = X.real * X.real + X.imag * X.imag
+    scale = want.max()
+    err = np.abs(got - want)
+    assert err.max() <= 1e-11 * scale, f"max abs err {err.max() / scale:.3e} of max"
+    big = want > 1e-6 * scale
+    assert np.max(err[big] / want[big]) < 1e-8
