@@ -67,7 +67,7 @@ template <int W, int T, int... Rs>
 __global__ __launch_bounds__(T) void k_rows_ct(const uint8_t* __restrict__ img, int H,
                                                const unsigned long long* __restrict__ sums,
                                                const double* __restrict__ k255g, const double2* __restrict__ twg,
-                                               double2* __restrict__ inter) {
+                                               double2* __restrict__ inter, int ablate) {
     using K = RowK<W, T, Rs...>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
@@ -132,15 +132,18 @@ __global__ __launch_bounds__(T) void k_rows_ct(const uint8_t* __restrict__ img, 
             }
         }
         const int prn = pair_of(s + 1);
-        if (prn < P) fetch(prn);
+        if (prn < P && !(ablate & 4)) fetch(prn);
         __syncthreads();
-        fft_lds<W, T, 1, Rs...>(buf, tw, tid);
+        if (!(ablate & 1)) fft_lds<W, T, 1, Rs...>(buf, tw, tid);
         constexpr int WF = W / 2 + 1;
-        for (int k = tid; k < WF; k += T) {
+        // lane pairs: lane 2j stores row y0's A[k], lane 2j+1 row y0+1's B[k] --
+        // one store instruction covers 32 columns x 32 contiguous bytes
+        for (int i = tid; i < 2 * WF && !(ablate & 2); i += T) {
+            const int k = i >> 1, second = i & 1;
             const double2 zk = buf[k], zm = buf[k == 0 ? 0 : W - k];
-            double2* o = inter + (size_t)k * H + y0;
-            o[0] = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-            if (two) o[1] = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+            const double2 o = second ? make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x))
+                                     : make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+            if (!second || two) inter[(size_t)k * H + y0 + second] = o;
         }
         __syncthreads();
         s++;
@@ -171,7 +174,8 @@ template <int H, int T, int... Rs>
 __global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter, int wf,
                                                const uint16_t* __restrict__ binmap, int nbins,
                                                double* __restrict__ bin_sums, double* __restrict__ fmax_part,
-                                               const double2* __restrict__ twg, double* __restrict__ dbg) {
+                                               const double2* __restrict__ twg, double* __restrict__ dbg,
+                                               int ablate) {
     using K = ColK<H, T, Rs...>;
     using L = typename K::L;
     constexpr int R = K::R;
@@ -206,9 +210,9 @@ __global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter
         const uint16_t* bcol = binmap + (size_t)col * H + tid * K::E;
 #pragma unroll
         for (int j = 0; j < K::E; j++) bm[j] = (H % K::E == 0 && K::E * T == H) || tid * K::E + j < H ? bcol[j] : 0;
-        if (col + 1 < c1) fetch(col + 1);
+        if (col + 1 < c1 && !(ablate & 4)) fetch(col + 1);
         __syncthreads();
-        K::PL::all_but_last(buf, tw, tid);
+        if (!(ablate & 1)) K::PL::all_but_last(buf, tw, tid);
         double2 v[L::ROUNDS][R];
         L::load(buf, v, tid);
         L::compute(v, tw + K::PL::last_tw_offset, tid);
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column)
-        {
+        if (!(ablate & 2)) {
             int cur = -1;
             double acc = 0.0;
 #pragma unroll
@@ -276,75 +280,112 @@ void allow_big_lds(K kernel) {
                               160 * 1024);
 }
 
-int row_grid() {
-    const int g = (2 * num_cus()) / 32 * 32;
-    return g > 32 ? g : 32;
+// resident blocks per CU x CUs (the persistent grids)
+template <typename K>
+int resident_grid(K kernel, int threads, size_t lds) {
+    allow_big_lds(kernel);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess || nb < 1) nb = 1;
+    return nb * num_cus();
 }
 
 template <int W, int T, int... Rs>
 hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, const double* k255,
                    const double2* tw, double2* inter, hipStream_t st) {
-    static bool once = (allow_big_lds(k_rows_ct<W, T, Rs...>), true);
-    (void)once;
     const size_t lds = RowK<W, T, Rs...>::lds;
-    hipLaunchKernelGGL((k_rows_ct<W, T, Rs...>), dim3(row_grid()), dim3(T), lds, st, img, H, sums, k255, tw, inter);
+    static const int grid = [&] {
+        const int g = resident_grid(k_rows_ct<W, T, Rs...>, T, lds) / 32 * 32;   // schedule needs % 32
+        return g > 32 ? g : 32;
+    }();
+    hipLaunchKernelGGL((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
+                       g_ablate);
     return hipGetLastError();
+}
+
+template <int H, int T, int... Rs>
+int cols_grid(int wf, int nbins) {
+    const int g = resident_grid(k_cols_ct<H, T, Rs...>, T, ColK<H, T, Rs...>::lds(nbins));
+    return wf < g ? wf : g;
 }
 
 template <int H, int T, int... Rs>
 hipError_t cols_ct(const double2* inter, int wf, const uint16_t* binmap, int nbins, double* bin_sums,
                    double* fmax_part, const double2* tw, double* dbg, hipStream_t st) {
-    static bool once = (allow_big_lds(k_cols_ct<H, T, Rs...>), true);
-    (void)once;
     const size_t lds = ColK<H, T, Rs...>::lds(nbins);
-    hipLaunchKernelGGL((k_cols_ct<H, T, Rs...>), dim3(fft_cols_ct_blocks(H, wf)), dim3(T), lds, st, inter, wf, binmap,
-                       nbins, bin_sums, fmax_part, tw, dbg);
+    hipLaunchKernelGGL((k_cols_ct<H, T, Rs...>), dim3(cols_grid<H, T, Rs...>(wf, nbins)), dim3(T), lds, st, inter,
+                       wf, binmap, nbins, bin_sums, fmax_part, tw, dbg, g_ablate);
     return hipGetLastError();
 }
 
+// the selected variant of length n, else variant 0
+#define PHD_PICK(LIST, n, rows, BODY)                                          \
+    do {                                                                       \
+        const int want_ = ct_variant(rows);                                    \
+        bool have_ = false;                                                    \
+        _Pragma("clang diagnostic push")                                       \
+        LIST(PHD_HAVE)                                                         \
+        _Pragma("clang diagnostic pop")                                        \
+        const int v_ = have_ ? want_ : 0;                                      \
+        LIST(BODY)                                                             \
+    } while (0)
+#define PHD_HAVE(N, V, T, ...) if (n_ == N && V == want_) have_ = true;
+
 }  // namespace
 
+int ct_variant(bool rows) {
+    static const int vr = getenv("PHD_CT_ROWS_VARIANT") ? atoi(getenv("PHD_CT_ROWS_VARIANT")) : 0;
+    static const int vc = getenv("PHD_CT_COLS_VARIANT") ? atoi(getenv("PHD_CT_COLS_VARIANT")) : 0;
+    return rows ? vr : vc;
+}
+
 bool ct_rows_plan(int w, std::vector<int>* radices) {
-#define PHD_X(N, T, ...)                             \
-    if (w == N) {                                    \
-        if (radices) *radices = std::vector<int>{__VA_ARGS__}; \
-        return true;                                 \
+    const int n_ = w;
+#define PHD_X(N, V, T, ...)                                          \
+    if (n_ == N && V == v_) {                                        \
+        if (radices) *radices = std::vector<int>{__VA_ARGS__};       \
+        return true;                                                 \
     }
-    PHD_CT_ROWS(PHD_X)
+    PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
 #undef PHD_X
     return false;
 }
 
 bool ct_cols_plan(int h, std::vector<int>* radices) {
-#define PHD_X(N, T, ...)                             \
-    if (h == N) {                                    \
-        if (radices) *radices = std::vector<int>{__VA_ARGS__}; \
-        return true;                                 \
+    const int n_ = h;
+#define PHD_X(N, V, T, ...)                                          \
+    if (n_ == N && V == v_) {                                        \
+        if (radices) *radices = std::vector<int>{__VA_ARGS__};       \
+        return true;                                                 \
     }
-    PHD_CT_COLS(PHD_X)
+    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return false;
 }
 
 size_t fft_cols_ct_lds(int h, int nbins) {
-#define PHD_X(N, T, ...) \
-    if (h == N) return ColK<N, T, __VA_ARGS__>::lds(nbins);
-    PHD_CT_COLS(PHD_X)
+    const int n_ = h;
+#define PHD_X(N, V, T, ...) \
+    if (n_ == N && V == v_) return ColK<N, T, __VA_ARGS__>::lds(nbins);
+    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return 0;
 }
 
-int fft_cols_ct_blocks(int height, int wf) {
-    (void)height;
-    const int g = 2 * num_cus();
-    return wf < g ? wf : g;
+int fft_cols_ct_blocks(int height, int wf, int nbins) {
+    const int n_ = height;
+#define PHD_X(N, V, T, ...) \
+    if (n_ == N && V == v_) return cols_grid<N, T, __VA_ARGS__>(wf, nbins);
+    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+#undef PHD_X
+    return 0;
 }
 
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
                               const double* k255, const double2* tw, double2* inter, hipStream_t st) {
-#define PHD_X(N, T, ...) \
-    if (width == N) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, st);
-    PHD_CT_ROWS(PHD_X)
+    const int n_ = width;
+#define PHD_X(N, V, T, ...) \
+    if (n_ == N && V == v_) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, st);
+    PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
 #undef PHD_X
     return hipErrorInvalidValue;
 }
@@ -352,9 +393,10 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
                               double* bin_sums, double* fmax_part, const double2* tw, double* dbg,
                               hipStream_t st) {
-#define PHD_X(N, T, ...) \
-    if (height == N) return cols_ct<N, T, __VA_ARGS__>(inter, wf, binmap, nbins, bin_sums, fmax_part, tw, dbg, st);
-    PHD_CT_COLS(PHD_X)
+    const int n_ = height;
+#define PHD_X(N, V, T, ...) \
+    if (n_ == N && V == v_) return cols_ct<N, T, __VA_ARGS__>(inter, wf, binmap, nbins, bin_sums, fmax_part, tw, dbg, st);
+    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return hipErrorInvalidValue;
 }

@@ -25,25 +25,21 @@ constexpr int kK1Threads = 1024;             // K1 block: 16 waves over one kChu
 struct K1Lds {
     static constexpr int k255 = 0;           // 256 doubles
     static constexpr int ent = 2048;         // 256 ClsEnt (16 B)
-    static constexpr int red = 6144;         // 16 waves x 8 x u64
-    static constexpr int qn = 7168;          // 2 ints (+pad)
-    static constexpr int si8 = 7184;         // 256 x 256 int8 saturation classes
-    static constexpr int queue = si8 + 65536;   // kQueue x u16 (pixel offset in the chunk)
-    static constexpr int hist = queue + 2 * kQueue;   // tl x u32 (K1: 3 x tl)
+    static constexpr int sthr = 6144;        // 256 x uint4 saturation-class thresholds
+    static constexpr int red = 10240;        // 16 waves x 8 x u64
+    static constexpr int qn = 11264;         // 2 ints (+pad)
+    static constexpr int queue = 11280;      // kQueue x u16 (pixel offset in the chunk)
+    static constexpr int hist = queue + 2 * kQueue;   // K1: 2 x (tl+1) x C lane copies + tl; K3: rules, sums
 };
 static_assert(sizeof(ClsEnt) == 16, "ClsEnt is one 16-B LDS read");
 
 __device__ __forceinline__ void stage_tables(unsigned char* smem, const double* __restrict__ k255g,
-                                             const ClassTables* __restrict__ tabs, bool with_si8 = true) {
+                                             const ClassTables* __restrict__ tabs) {
     const int tid = threadIdx.x;
-    if (tid < 256) {
-        reinterpret_cast<double*>(smem + K1Lds::k255)[tid] = k255g[tid];
-        reinterpret_cast<ClsEnt*>(smem + K1Lds::ent)[tid] = tabs->ent[tid];
-    }
-    if (with_si8) {
-        const uint4* src = reinterpret_cast<const uint4*>(tabs->si8);
-        uint4* dst = reinterpret_cast<uint4*>(smem + K1Lds::si8);
-        for (int i = tid; i < 65536 / 16; i += blockDim.x) dst[i] = src[i];
+    for (int i = tid; i < 256; i += blockDim.x) {
+        reinterpret_cast<double*>(smem + K1Lds::k255)[i] = k255g[i];
+        reinterpret_cast<ClsEnt*>(smem + K1Lds::ent)[i] = tabs->ent[i];
+        reinterpret_cast<uint4*>(smem + K1Lds::sthr)[i] = reinterpret_cast<const uint4*>(tabs->sthr)[i];
     }
 }
 
@@ -94,14 +90,11 @@ __device__ __forceinline__ void hist_add(unsigned* lds, int g) {
 #ifndef PHD_K1_ABLATE
 #define PHD_K1_ABLATE 0        // K1 ablation mask for timing builds (8 classify, 16 hist, 32 sat, 128 atomics)
 #endif
-#ifndef PHD_SAT_MODE
-#define PHD_SAT_MODE 0
-#endif
 #ifndef PHD_K1_MINWAVES
 #define PHD_K1_MINWAVES 8        // waves/SIMD the statistics-only K1 is sized for (2 blocks/CU)
 #endif
 #ifndef PHD_K1_MINWAVES_HIST
-#define PHD_K1_MINWAVES_HIST 4   // histogram K1: its 64 KiB table allows 1 block/CU anyway
+#define PHD_K1_MINWAVES_HIST 4   // histogram K1 (1024 threads, <= 128 VGPRs: one block per CU)
 #endif
 
 // Per-image outputs of a batch: image i's records sit at i * stride bytes.
@@ -140,18 +133,6 @@ __device__ __forceinline__ void load_group(const uint8_t* ip, long p0, bool ok, 
     }
 }
 
-// hist_add for a fully active wave whose g are all valid slots (K1's deferred
-// pixels count into a dummy slot): one atomic per wave when the whole wave
-// hits one group (flat regions), else one per lane.
-__device__ __forceinline__ void hist_add_full(unsigned* lds, int g) {
-    const int g0 = __builtin_amdgcn_readfirstlane(g);
-    if (__builtin_amdgcn_ballot_w64(g != g0) == 0) {
-        if (lane_id() == 0) atomicAdd(&lds[g0], 64u);
-    } else {
-        atomicAdd(&lds[g], 1u);
-    }
-}
-
 // K1 for downsample_rate == 1, over a whole batch of same-size images in one
 // launch: channel moments, sum(s) and (kHist) the group histogram.
 //
@@ -165,6 +146,8 @@ __device__ __forceinline__ void hist_add_full(unsigned* lds, int g) {
 // classify through classify(); the few near a bin edge are queued and
 // classified exactly after the chunk's stream so waves stay convergent.  The
 // next item's loads are issued before the current chunk's barriers.
+// The chunk counts have C = 1 << cshift lane-private copies (lane l adds to
+// copy l mod C), so the per-pixel LDS atomics never collide within a wave.
 // kHist == false is the rgb2hsv + statistics pass alone (S-bar and moments).
 //
 // Each thread owns kSteps groups of 4 pixels (12 bytes, one dwordx3) per
@@ -176,27 +159,28 @@ template <bool kHist, bool kAligned>
 __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_MINWAVES) void k_hsv_stats(
         const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
         const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, PaletteDev out, long a_stride,
-        long h_stride) {
+        long h_stride, int cshift) {
     constexpr int ablate = PHD_K1_ABLATE;   // compile-time ablation (timing builds only)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
+    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
+    const signed char* si8 = tabs->si8;                                 // global (s_partitions > 8 only)
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + K1Lds::red);
     int* qn = reinterpret_cast<int*>(smem + K1Lds::qn);
     unsigned short* queue = reinterpret_cast<unsigned short*>(smem + K1Lds::queue);
     const int tl = gp.tl;
     const int tl1 = tl + 1;                                             // + dummy slot (deferred pixels)
-    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);   // [2][tl1] chunk counts
-    unsigned* seg = lh + 2 * tl1;                                      // [tl] counts of the run
+    const int C = 1 << cshift, cm = C - 1;
+    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);   // [2][tl1][C] chunk counts
+    unsigned* seg = lh + 2 * tl1 * C;                                  // [tl] counts of the run
     const int tid = threadIdx.x;
+    const int mycopy = tid & cm;
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
-    stage_tables(smem, k255g, tabs, kHist);
-    if (!kHist && PHD_SAT_MODE == 1 && tid < 256) reinterpret_cast<double*>(smem + K1Lds::si8)[tid] = tabs->ent[tid].rinv;
-    if (!kHist && PHD_SAT_MODE == 2 && tid < 256) reinterpret_cast<float*>(smem + K1Lds::si8)[tid] = (float)tabs->ent[tid].rinv;
+    stage_tables(smem, k255g, tabs);
     if (kHist) {
-        for (int i = tid; i < 2 * tl1 + tl; i += kK1Threads) lh[i] = 0;
+        for (int i = tid; i < 2 * tl1 * C + tl; i += kK1Threads) lh[i] = 0;
         if (tid < 2) qn[tid] = 0;
     }
     __syncthreads();
@@ -226,7 +210,7 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
     int seg_c0 = c, par = 0;
     long seg_it0 = it0;
     for (long it = it0; it < it1; it++, par ^= 1) {
-        unsigned* ch = lh + par * tl1;
+        unsigned* ch = lh + par * tl1 * C;
         const long base = (long)c * kChunk;
         // one group (4 pixels) per iteration; the words rotate through
         // registers so the loop is not unrolled (bounded live state)
@@ -236,7 +220,6 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
         for (int st = 0; st < kSteps; st++) {
             const int o0 = 4 * tid + 4 * kK1Threads * st;     // offset in the chunk
             const unsigned cw[3] = {c0, c1, c2};
-            float s4 = 0.f;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int kr = px_byte(cw, 3 * i), kg = px_byte(cw, 3 * i + 1), kb = px_byte(cw, 3 * i + 2);
@@ -244,41 +227,17 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
                 qr += kr * kr; qg += kg * kg; qb += kb * kb;
                 if (kHist) {
                     double sv = 0.0;
-                    int g = (ablate & 8) ? (kr & 63) : classify(kr, kg, kb, ent, si8, gp, fc, sv);
+                    int g = (ablate & 8) ? (kr & 63) : classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
                     if (!(ablate & 32)) ssum += sv;
                     if (g == -2) {            // on a hue bin edge: classify exactly after the stream
                         queue[atomicAdd(&qn[par], 1)] = (unsigned short)(o0 + i);
                         g = tl;
                     }
-                    if (!(ablate & 16)) hist_add_full(ch, g);
+                    if (!(ablate & 16)) atomicAdd(&ch[(g << cshift) | mycopy], 1u);
                 } else {
-#if PHD_SAT_MODE == 0
                     if (!(ablate & 32)) ssum += sat_only(kr, kg, kb, ent);
-#elif PHD_SAT_MODE == 1
-                    {
-                        const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
-                        const double sv = (double)kd * reinterpret_cast<const double*>(si8)[kmx];
-                        ssum += (kmn == 0 && kd != 0) ? 0.999999 : sv;
-                    }
-#elif PHD_SAT_MODE == 2
-                    {
-                        const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
-                        const float sv = (float)kd * reinterpret_cast<const float*>(si8)[kmx];
-                        s4 += (kmn == 0 && kd != 0) ? 0.999999f : sv;
-                    }
-#else
-                    {
-                        const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
-                        const double k = (double)max(kmx, 1);
-                        double r = __builtin_amdgcn_rcp(k);
-                        r = fma(fma(-k, r, 1.0), r, r);
-                        const double sv = (double)kd * r;
-                        ssum += (kmn == 0 && kd != 0) ? 0.999999 : sv;
-                    }
-#endif
                 }
             }
-            if (PHD_SAT_MODE == 2) ssum += (double)s4;
             bits >>= 1;
             const bool okn = bits & 1;
             c0 = okn ? w[1][0] : 0u;
@@ -299,9 +258,9 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
                 qr += kr * kr; qg += kg * kg; qb += kb * kb;
                 double sv;
                 if (kHist) {
-                    int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+                    int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
                     if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
-                    atomicAdd(&ch[g], 1u);
+                    atomicAdd(&ch[g << cshift], 1u);
                 } else {
                     sv = sat_only(kr, kg, kb, ent);
                 }
@@ -326,25 +285,33 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
             const long pad = base + kChunk - full_end;
             if (pad > 0 && tid == 0) {
                 double sv;
-                atomicSub(&ch[classify(0, 0, 0, ent, si8, gp, fc, sv)], (unsigned)pad);
+                atomicSub(&ch[classify(0, 0, 0, ent, sthr, si8, gp, fc, sv) << cshift], (unsigned)pad);
             }
             const int nq = qn[par];
             for (int q = tid; q < nq; q += kK1Threads) {
                 const long p = base + queue[q];
-                atomicAdd(&ch[exact_group(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp)], 1u);
+                atomicAdd(&ch[(exact_group(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp) << cshift) | mycopy],
+                          1u);
             }
             __syncthreads();
+            // fold the C copies of each group (C consecutive lanes) with shuffles
             unsigned short* chunk_out = img_chunks(out, h_stride, cimg) + (long)cc * tl;
-            for (int i = tid; i < tl; i += kK1Threads) {
-                const unsigned n = ch[i];
-                chunk_out[i] = (unsigned short)n;
-                seg[i] += n;
-                ch[i] = 0;
+            const int ncopy = tl << cshift;
+            for (int i0 = tid; i0 < ((ncopy + kK1Threads - 1) & ~(kK1Threads - 1)); i0 += kK1Threads) {
+                unsigned n = 0;
+                if (i0 < ncopy) {
+                    n = ch[i0];
+                    ch[i0] = 0;
+                }
+                for (int o = 1; o < C; o <<= 1) n += __shfl_xor(n, o, 64);
+                if (i0 < ncopy && (i0 & cm) == 0) {
+                    const int g = i0 >> cshift;
+                    chunk_out[g] = (unsigned short)n;
+                    seg[g] += n;
+                }
             }
-            if (tid == 0) {
-                qn[par] = 0;
-                ch[tl] = 0;
-            }
+            if (tid < C) ch[(tl << cshift) + tid] = 0;        // the deferred-pixel slot
+            if (tid == 0) qn[par] = 0;
         }
         if (!more || img != cimg || it + 1 - seg_it0 == 4096) {
             // the run leaves image cimg (or its u32 moments could overflow):
@@ -431,11 +398,11 @@ __device__ unsigned long long block_excl_scan_k1_u64(unsigned long long x, unsig
 }
 
 // Exact group of a pixel: classify(), and the exact hue on a bin edge.
-__device__ __forceinline__ int exact_group_t(int kr, int kg, int kb, const ClsEnt* ent, const signed char* si8,
-                                             const double* k255, const GridParams& gp, const FastCls& fc,
-                                             double& s) {
-    int g = classify(kr, kg, kb, ent, si8, gp, fc, s);
-    if (g == -2) g = edge_group(kr, kg, kb, hue_exact(kr, kg, kb, k255), ent, si8, gp);
+__device__ __forceinline__ int exact_group_t(int kr, int kg, int kb, const ClsEnt* ent, const uint4* sthr,
+                                             const signed char* si8, const double* k255, const GridParams& gp,
+                                             const FastCls& fc, double& s) {
+    int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, s);
+    if (g == -2) g = edge_group(kr, kg, kb, hue_exact(kr, kg, kb, k255), ent, sthr, si8, gp, fc);
     return g;
 }
 
@@ -454,12 +421,13 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
+    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
+    const signed char* si8 = tabs->si8;
     int* scratch = reinterpret_cast<int*>(smem + K1Lds::red);          // 16 x u64
     int* misc = reinterpret_cast<int*>(smem + K1Lds::red + 256);       // chunk, rank, last chunk
     unsigned* found = reinterpret_cast<unsigned*>(smem + K1Lds::qn);
     const int tid = threadIdx.x;
-    stage_tables(smem, k255g, tabs, true);
+    stage_tables(smem, k255g, tabs);
     const int img = entries[blockIdx.x].x, g = entries[blockIdx.x].y;
     const uint8_t* ip = imgs[img];
     GroupRule* rules = reinterpret_cast<GroupRule*>(reinterpret_cast<char*>(rules0) + img * b_stride);
@@ -510,7 +478,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
                     continue;
                 }
                 double sv;
-                if (exact_group_t(kr, kg, kb, ent, si8, k255, gp, fc, sv) == g) hits |= 1u << (4 * st + i);
+                if (exact_group_t(kr, kg, kb, ent, sthr, si8, k255, gp, fc, sv) == g) hits |= 1u << (4 * st + i);
             }
         }
         if (tid == 0) *found = 0;
@@ -556,27 +524,37 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
 // src/color_quantization.c:529-558): sum wrap(h + off), sum s, sum v, count.
 // Persistent blocks walk contiguous runs of (image, chunk) items like K1;
 // per image the keep rules are packed into LDS as {slot, cut, last}: a pixel
-// of a slotted group is kept when its index < cut or == last.  Sums stay in
-// LDS per slot and go to HBM with one atomic per slot and field per run.
+// of a slotted group is kept when its index < cut or == last.  The sums have
+// C = 1 << cshift lane-private copies per slot (lane l adds to copy l mod C):
+// the fp64 LDS atomics of one wave hit distinct addresses (and, for C = 32,
+// distinct banks), whatever the image.  Per image, the copies are folded and
+// go to HBM with one atomic per slot and field.
 template <bool kAligned>
 __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
         const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
         const ClassTables* __restrict__ tabs, const double* __restrict__ k255g,
         const GroupRule* __restrict__ rules0, const double* __restrict__ off0, long b_stride,
-        const int* __restrict__ nslots_img, int max_slots, double* out0, long c_stride) {
+        const int* __restrict__ nslots_img, int max_slots, double* out0, long c_stride, int cshift) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
+    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
+    const signed char* si8 = tabs->si8;
     const int tl = gp.tl;
+    const int C = 1 << cshift, cm = C - 1;
     uint4* rec = reinterpret_cast<uint4*>(smem + K1Lds::queue);        // [tl] {slot, cut, last, -}
     double* off = reinterpret_cast<double*>(rec + tl);                 // [max_slots]
-    double* acc = off + max_slots;                                     // [3][max_slots] h, s, v
-    unsigned* cnt = reinterpret_cast<unsigned*>(acc + 3 * max_slots);  // [max_slots]
+    double* acc = off + max_slots;                                     // [3][max_slots][C] h, s, v
+    unsigned* cnt = reinterpret_cast<unsigned*>(acc + 3 * max_slots * C);   // [max_slots][C]
     const int tid = threadIdx.x;
+    const int mycopy = tid & cm;
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
-    stage_tables(smem, k255g, tabs, true);
+    stage_tables(smem, k255g, tabs);
+    for (int i = tid; i < max_slots * C; i += kK1Threads) {
+        acc[i] = acc[max_slots * C + i] = acc[2 * max_slots * C + i] = 0.0;
+        cnt[i] = 0;
+    }
 
     constexpr int kSteps = kChunk / (4 * kK1Threads);
     const long full_end = npix & ~3L;
@@ -597,11 +575,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                 q.w = 0;
                 rec[i] = q;
             }
-            for (int i = tid; i < ns; i += kK1Threads) {
-                off[i] = offi[i];
-                acc[i] = acc[max_slots + i] = acc[2 * max_slots + i] = 0.0;
-                cnt[i] = 0;
-            }
+            for (int i = tid; i < ns; i += kK1Threads) off[i] = offi[i];
             cur = img;
             __syncthreads();
         }
@@ -625,53 +599,58 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
             for (int i = 0; i < 4; i++) {
                 const int kr = px_byte(cw, 3 * i), kg = px_byte(cw, 3 * i + 1), kb = px_byte(cw, 3 * i + 2);
                 double sv;
-                int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
-                const double hx = hue_exact(kr, kg, kb, k255);
-                if (g == -2) g = edge_group(kr, kg, kb, hx, ent, si8, gp);
-                const uint4 q = rec[g];
+                int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
+                const uint4 q = rec[g == -2 ? 0 : g];
                 const unsigned idx = (unsigned)(p0 + i);
-                const bool kept = okg && (int)q.x >= 0 && (idx < q.y || idx == q.z);
-                const int sl = kept ? (int)q.x : -1;
-                double tp = hx + off[kept ? sl : 0];
-                tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
-                const double vv = v_of(max(kr, max(kg, kb)), k255);
-                const int s0 = __builtin_amdgcn_readfirstlane(sl);
-                if (__builtin_amdgcn_ballot_w64(sl != s0) == 0) {
-                    if (s0 >= 0) {
-                        const double th = wave_sum(tp), ts = wave_sum(sv), tv = wave_sum(vv);
-                        if (lane_id() == 0) {
-                            atomicAdd(&acc[s0], th);
-                            atomicAdd(&acc[max_slots + s0], ts);
-                            atomicAdd(&acc[2 * max_slots + s0], tv);
-                            atomicAdd(&cnt[s0], 64u);
+                bool kept = okg && (int)q.x >= 0 && (idx < q.y || idx == q.z);
+                if (g == -2 || kept) {
+                    const double hx = hue_exact(kr, kg, kb, k255);
+                    if (g == -2) {                           // on a hue bin edge: the exact group
+                        g = edge_group(kr, kg, kb, hx, ent, sthr, si8, gp, fc);
+                        const uint4 r = rec[g];
+                        kept = okg && (int)r.x >= 0 && (idx < r.y || idx == r.z);
+                        if (kept) {
+                            const int sl = (int)r.x;
+                            double tp = hx + off[sl];
+                            tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+                            const int a = (sl << cshift) | mycopy;
+                            atomicAdd(&acc[a], tp);
+                            atomicAdd(&acc[max_slots * C + a], sv);
+                            atomicAdd(&acc[2 * max_slots * C + a], v_of(max(kr, max(kg, kb)), k255));
+                            atomicAdd(&cnt[a], 1u);
                         }
+                    } else {
+                        const int sl = (int)q.x;
+                        double tp = hx + off[sl];
+                        tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+                        const int a = (sl << cshift) | mycopy;
+                        atomicAdd(&acc[a], tp);
+                        atomicAdd(&acc[max_slots * C + a], sv);
+                        atomicAdd(&acc[2 * max_slots * C + a], v_of(max(kr, max(kg, kb)), k255));
+                        atomicAdd(&cnt[a], 1u);
                     }
-                } else if (sl >= 0) {
-                    atomicAdd(&acc[sl], tp);
-                    atomicAdd(&acc[max_slots + sl], sv);
-                    atomicAdd(&acc[2 * max_slots + sl], vv);
-                    atomicAdd(&cnt[sl], 1u);
                 }
             }
         }
         if (base + kChunk >= npix && tid == 0) {
-            // the partial final group of the image: one lane, plain atomics
+            // the partial final group of the image: one lane
             for (long p = full_end; p < npix; p++) {
                 const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
                 double sv;
                 const double hx = hue_exact(kr, kg, kb, k255);
-                int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
-                if (g == -2) g = edge_group(kr, kg, kb, hx, ent, si8, gp);
+                int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
+                if (g == -2) g = edge_group(kr, kg, kb, hx, ent, sthr, si8, gp, fc);
                 const uint4 q = rec[g];
                 const unsigned idx = (unsigned)p;
                 if ((int)q.x >= 0 && (idx < q.y || idx == q.z)) {
                     const int sl = (int)q.x;
                     double tp = hx + off[sl];
                     tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
-                    atomicAdd(&acc[sl], tp);
-                    atomicAdd(&acc[max_slots + sl], sv);
-                    atomicAdd(&acc[2 * max_slots + sl], v_of(max(kr, max(kg, kb)), k255));
-                    atomicAdd(&cnt[sl], 1u);
+                    const int a = sl << cshift;
+                    atomicAdd(&acc[a], tp);
+                    atomicAdd(&acc[max_slots * C + a], sv);
+                    atomicAdd(&acc[2 * max_slots * C + a], v_of(max(kr, max(kg, kb)), k255));
+                    atomicAdd(&cnt[a], 1u);
                 }
             }
         }
@@ -683,14 +662,25 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
         if (it + 1 == it1 || img != cimg) {                  // flush image cimg's sums
             __syncthreads();
             double* out = reinterpret_cast<double*>(reinterpret_cast<char*>(out0) + cimg * c_stride);
-            for (int i = tid; i < ns; i += kK1Threads) {
-                const unsigned n = cnt[i];
-                if (n) {
-                    atomicAdd(&out[4 * i + 0], acc[i]);
-                    atomicAdd(&out[4 * i + 1], acc[max_slots + i]);
-                    atomicAdd(&out[4 * i + 2], acc[2 * max_slots + i]);
-                    atomicAdd(&out[4 * i + 3], (double)n);
+            // one (field, slot, copy) per lane; the C copies of a slot are
+            // consecutive lanes and fold with shuffles
+            const int ncopy = ns << cshift;
+            const int total = 4 * ncopy;
+            for (int i0 = tid; i0 < ((total + kK1Threads - 1) & ~(kK1Threads - 1)); i0 += kK1Threads) {
+                const int f = i0 / max(ncopy, 1), j = i0 - f * ncopy;
+                double a = 0.0;
+                if (i0 < total) {
+                    if (f < 3) {
+                        double* src = &acc[f * max_slots * C + j];
+                        a = *src;
+                        *src = 0.0;
+                    } else {
+                        a = (double)cnt[j];
+                        cnt[j] = 0;
+                    }
                 }
+                for (int o = 1; o < C; o <<= 1) a += __shfl_xor(a, o, 64);
+                if (i0 < total && (j & cm) == 0 && a != 0.0) atomicAdd(&out[4 * (j >> cshift) + f], a);
             }
             __syncthreads();
         }
@@ -705,7 +695,8 @@ __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const signed char* si8 = reinterpret_cast<const signed char*>(smem + K1Lds::si8);
+    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
+    const signed char* si8 = tabs->si8;
     double* red = reinterpret_cast<double*>(smem + K1Lds::red);
     unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);
     const int tid = threadIdx.x;
@@ -719,7 +710,7 @@ __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__
         const long p = src_pixel(j, width, ds, nw);
         const int kr = img[3 * p], kg = img[3 * p + 1], kb = img[3 * p + 2];
         double sv;
-        int g = classify(kr, kg, kb, ent, si8, gp, fc, sv);
+        int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
         ssum += sv;
         if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
         hist_add(lh, g);
@@ -956,7 +947,7 @@ __global__ void k_debug_hsv(const uint8_t* __restrict__ img, long n, GridParams 
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const int kr = img[3 * i], kg = img[3 * i + 1], kb = img[3 * i + 2];
         double sv;
-        int g = classify(kr, kg, kb, tabs->ent, tabs->si8, gp, fc, sv);
+        int g = classify(kr, kg, kb, tabs->ent, reinterpret_cast<const uint4*>(tabs->sthr), tabs->si8, gp, fc, sv);
         if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
         gid[i] = g;
         if (hsv) {
@@ -1006,8 +997,23 @@ static inline long hsv_pixels(int height, int width, int ds, int* nw) {
     return (long)(short)hh * (short)ww;   // rgb2hsv's short dimensions, image_processing.c:378-383
 }
 
+// lane-private copies of K1's chunk counts: as many as fit 40 KiB (<= 32)
+int k1_cshift(int tl) {
+    int c = 5;
+    while (c > 0 && 2 * (size_t)(tl + 1) * (4u << c) > 40 * 1024) c--;
+    return c;
+}
+
+// ... and of K3's slot sums (28 B per copy): <= 96 KiB
+int k3_cshift(int max_slots) {
+    int c = 5;
+    while (c > 0 && (size_t)max_slots * (28u << c) > 96 * 1024) c--;
+    return c;
+}
+
 size_t hsv_stats_lds(const GridParams& gp, bool hist) {
-    return hist ? K1Lds::hist + sizeof(unsigned) * (3 * (size_t)gp.tl + 2) : (size_t)K1Lds::si8 + 2048;
+    return hist ? K1Lds::hist + sizeof(unsigned) * (2 * ((size_t)gp.tl + 1) * (1u << k1_cshift(gp.tl)) + gp.tl)
+                : (size_t)K1Lds::red + 1024;
 }
 
 hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width,
@@ -1028,7 +1034,7 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
             attr = true;                                                                                      \
         }                                                                                                     \
         hipLaunchKernelGGL((k_hsv_stats<H, A>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix, nchunks, \
-                           nitems, gp, fc, tabs, k255, out0, a_stride, h_stride);                             \
+                           nitems, gp, fc, tabs, k255, out0, a_stride, h_stride, k1_cshift(gp.tl));           \
     } while (0)
     if (hist) {
         if (aligned) PHD_K1_LAUNCH(true, true);
@@ -1086,7 +1092,7 @@ hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds
 }
 
 size_t palette_sums_b_lds(int tl, int max_slots) {
-    return (size_t)K1Lds::queue + 16 * (size_t)tl + 36 * (size_t)max_slots;
+    return (size_t)K1Lds::queue + 16 * (size_t)tl + 8 * (size_t)max_slots + (size_t)max_slots * (28u << k3_cshift(max_slots));
 }
 
 hipError_t launch_cutoffs_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n, int height,
@@ -1139,7 +1145,7 @@ hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t
         }                                                                                                   \
         hipLaunchKernelGGL((k_palette_sums_b<A>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix,        \
                            nchunks, nitems, gp, fc, tabs, k255, rules0, off0, b_stride, nslots_img,         \
-                           max_slots, out0, c_stride);                                                      \
+                           max_slots, out0, c_stride, k3_cshift(max_slots));                                \
     } while (0)
     if (aligned) PHD_K3_LAUNCH(true);
     else PHD_K3_LAUNCH(false);

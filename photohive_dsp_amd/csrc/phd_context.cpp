@@ -155,7 +155,7 @@ const FftPlanHost* get_plan(Context* c, int n) {
 }
 
 const double2* get_ct_twiddles(Context* c, int n, bool rows) {
-    const auto key = std::make_pair(n, rows ? 1 : 0);
+    const auto key = std::make_pair(n, (rows ? 1 : 0) + 2 * ct_variant(rows));
     auto it = c->ct_tw.find(key);
     if (it != c->ct_tw.end()) return it->second;
     std::vector<int> rad;
@@ -198,7 +198,7 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         s->tw_r = get_ct_twiddles(c, width, true);
         s->tw_c = get_ct_twiddles(c, height, false);
         if (!s->tw_r || !s->tw_c) return false;
-        s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1);
+        s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
         return true;
     }
     s->prow = get_plan(c, width);

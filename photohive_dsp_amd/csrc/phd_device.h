@@ -55,14 +55,29 @@ __device__ __forceinline__ int group_of(const GridParams& gp, double h, double s
 // gap to any integer and truncates to floor(N/D) exactly.  When D divides N
 // and num is not 0 or +-d, the reference's double hue may round either side
 // of the edge: those pixels (-2) take the fp64 path.  Select-only code.
-__device__ __forceinline__ int classify(int kr, int kg, int kb, const ClsEnt* ent, const signed char* si8,
-                                        const GridParams& gp, const FastCls& F, double& s_out) {
+// Si of arm_octree (src/color_quantization.c:140) for (kmax, kd): the threshold
+// count of ClassTables::sthr (LDS copy), or the full table in global memory.
+__device__ __forceinline__ int si_of(int kmx, int kd, const uint4* sthr, const signed char* si8g,
+                                     const FastCls& F) {
+    if (F.use_thr) {
+        const uint4 t = sthr[kmx];
+        const unsigned u = (unsigned)kd;
+        return -1 + (int)(u >= (t.x & 0xFFFFu)) + (int)(u >= (t.x >> 16)) + (int)(u >= (t.y & 0xFFFFu)) +
+               (int)(u >= (t.y >> 16)) + (int)(u >= (t.z & 0xFFFFu)) + (int)(u >= (t.z >> 16)) +
+               (int)(u >= (t.w & 0xFFFFu)) + (int)(u >= (t.w >> 16));
+    }
+    return si8g[(kmx << 8) | kd];
+}
+
+__device__ __forceinline__ int classify(int kr, int kg, int kb, const ClsEnt* ent, const uint4* sthr,
+                                        const signed char* si8g, const GridParams& gp, const FastCls& F,
+                                        double& s_out) {
     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
     const ClsEnt e = ent[kmx];
     // s exactly as rgb2hsv up to the last ulp: 0 (d == 0), 0.999999 (d == max), else d / max
     const double s = (double)kd * e.rinv;
     s_out = (kmn == 0 && kd != 0) ? 0.999999 : s;
-    const int si = si8[(kmx << 8) | kd];
+    const int si = si_of(kmx, kd, sthr, si8g, F);
     // hue bin
     const bool isr = kr == kmx, isg = kg == kmx;
     const int a = isr ? kg : (isg ? kb : kr), b = isr ? kb : (isg ? kr : kg);
@@ -97,10 +112,10 @@ __device__ __forceinline__ double hue_exact(int kr, int kg, int kb, const double
 
 // The group of a pixel that classify() left on a hue bin edge (-2: a colour
 // pixel), from its exact hue: arm_octree's (int)(h / Lh).
-__device__ __forceinline__ int edge_group(int kr, int kg, int kb, double h, const ClsEnt* ent,
-                                          const signed char* si8, const GridParams& gp) {
+__device__ __forceinline__ int edge_group(int kr, int kg, int kb, double h, const ClsEnt* ent, const uint4* sthr,
+                                          const signed char* si8g, const GridParams& gp, const FastCls& F) {
     const int kmx = max(kr, max(kg, kb)), kd = kmx - min(kr, min(kg, kb));
-    const int si = si8[(kmx << 8) | kd];
+    const int si = si_of(kmx, kd, sthr, si8g, F);
     const int vi = (ent[kmx].vpack << 16) >> 16;
     const int hi = (int)(h / gp.Lh);
     return (hi * gp.sp + si) * gp.vp + vi;

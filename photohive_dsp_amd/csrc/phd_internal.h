@@ -31,6 +31,7 @@ struct GridParams {
 // bin edge (where the reference's double rounding decides) take the fp64 path.
 struct FastCls {
     int lh;                    // Lh = 360 / h_partitions (integer division, :41)
+    int use_thr;               // Si from ClassTables::sthr (s_partitions <= 8), else si8 in global memory
 };
 struct ClsEnt {                // per max channel value k (16 B: one LDS read)
     double rinv;               // 1 / k (k > 0; 0 for k == 0), saturation sums
@@ -38,8 +39,12 @@ struct ClsEnt {                // per max channel value k (16 B: one LDS read)
                                // high 16 bits: gray group id of v(k)
     int pad;
 };
-struct ClassTables {           // device copy, staged into LDS by the kernels
+struct ClassTables {           // device copy; ent and sthr are staged into LDS by the kernels
     ClsEnt ent[256];
+    // Si is non-decreasing in kd = kmax - kmin for a fixed kmax, so it is -1 plus
+    // the number of thresholds kd reaches: sthr[kmax][j] packs the smallest kd
+    // with Si >= 2i and >= 2i+1 (low / high 16 bits; 0xFFFF = never).
+    unsigned sthr[256][4];
     signed char si8[256 * 256];   // [kmax][kmax - kmin]: Si of s, -1 when s < gray_thresh
 };
 
@@ -132,15 +137,30 @@ hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPl
 int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds, int* lds_bins);
 
 // ---- compile-time FFT plans (fft_ct.hip / fft_engine.h) ------------------------
-// X(length, threads per block, radices...).  The first radix is odd (LDS
-// bank-conflict-free first pass, fft_engine.h).  Rows need length % 4 == 0.
-#define PHD_CT_ROWS(X) X(4000, 256, 25, 16, 10)
-#define PHD_CT_COLS(X) X(3000, 256, 15, 20, 10)
+// X(length, variant, threads per block, radices...).  Variant 0 is production;
+// PHD_CT_ROWS_VARIANT / PHD_CT_COLS_VARIANT select another for tuning runs.
+// The first radix is odd (LDS bank-conflict-free first pass, fft_engine.h).
+// Rows need length % 4 == 0.
+#define PHD_CT_ROWS(X)              \
+    X(4000, 0, 256, 25, 16, 10)     \
+    X(4000, 1, 256, 25, 20, 8)      \
+    X(4000, 2, 512, 25, 16, 10)     \
+    X(4000, 3, 400, 25, 16, 10)     \
+    X(4000, 4, 320, 25, 16, 10)
+#define PHD_CT_COLS(X)              \
+    X(3000, 0, 256, 15, 20, 10)     \
+    X(3000, 1, 256, 25, 12, 10)     \
+    X(3000, 2, 320, 15, 20, 10)     \
+    X(3000, 3, 512, 15, 20, 10)     \
+    X(3000, 4, 192, 25, 12, 10)     \
+    X(3000, 5, 300, 25, 12, 10)
+int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);
 bool ct_cols_plan(int h, std::vector<int>* radices);
 size_t fft_cols_ct_lds(int height, int nbins);
-int fft_cols_ct_blocks(int height, int wf);
+// persistent grid of the column kernel (= entries of fmax_part)
+int fft_cols_ct_blocks(int height, int wf, int nbins);
 // tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built)
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
                               const double* k255, const double2* tw, double2* inter, hipStream_t st);

@@ -105,6 +105,21 @@ void make_class_tables(const GridParams& g, FastCls* fc, ClassTables* t) {
         }
     }
     fc->lh = 360 / g.hp;
+    // threshold form of si8 (see ClassTables::sthr); valid while Si is
+    // non-decreasing in kd and takes at most 8 non-negative values
+    bool mono = g.sp <= 8;
+    for (int k = 0; k < 256 && mono; k++) {
+        unsigned short thr[8];
+        for (int j = 0; j < 8; j++) thr[j] = 0xFFFF;
+        for (int kd = 0; kd <= k; kd++) {
+            const int si = t->si8[k * 256 + kd];
+            if (kd > 0 && si < t->si8[k * 256 + kd - 1]) mono = false;
+            for (int j = 0; j <= si && j < 8; j++)
+                if (thr[j] == 0xFFFF) thr[j] = (unsigned short)kd;
+        }
+        for (int i = 0; i < 4; i++) t->sthr[k][i] = (unsigned)thr[2 * i] | ((unsigned)thr[2 * i + 1] << 16);
+    }
+    fc->use_thr = mono ? 1 : 0;
 }
 
 namespace {

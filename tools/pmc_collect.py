@@ -19,12 +19,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"k_hsv_stats": "hsv_stats", "k_fft_rows": "fft_rows", "k_fft_cols": "fft_cols",
+         "k_rows_ct": "fft_rows", "k_cols_ct": "fft_cols", "k_cutoffs_b": "palette_cutoffs",
+         "k_palette_sums_b": "palette_sums",
          "k_cutoffs": "palette_cutoffs", "k_palette_sums": "palette_sums", "k_sharp_pass": "sharpness"}
 
 
 def short(name):
     for k, v in SHORT.items():
-        if k + "(" in name or name.endswith(k):
+        if k + "(" in name or k + "<" in name or name.endswith(k):
             return v
     return None
 
