@@ -67,8 +67,9 @@ template <int W, int T, int... Rs>
 __global__ __launch_bounds__(T) void k_rows_ct(const uint8_t* __restrict__ img, int H,
                                                const unsigned long long* __restrict__ sums,
                                                const double* __restrict__ k255g, const double2* __restrict__ twg,
-                                               double2* __restrict__ inter, int ablate) {
+                                               double2* __restrict__ inter, int ablate_arg) {
     using K = RowK<W, T, Rs...>;
+    const int ablate = PHD_ABL(ablate_arg);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
     double2* tw = buf + W;
@@ -175,8 +176,9 @@ __global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter
                                                const uint16_t* __restrict__ binmap, int nbins,
                                                double* __restrict__ bin_sums, double* __restrict__ fmax_part,
                                                const double2* __restrict__ twg, double* __restrict__ dbg,
-                                               int ablate) {
+                                               int ablate_arg) {
     using K = ColK<H, T, Rs...>;
+    const int ablate = PHD_ABL(ablate_arg);
     using L = typename K::L;
     constexpr int R = K::R;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -20,16 +20,13 @@ namespace phd {
 namespace {
 
 // LDS carve of K1 (one dynamic array, 16-B aligned base: no static __shared__).
-constexpr int kQueue = kChunk;               // deferred exact-path pixels (u16 offsets): never overflows
 constexpr int kK1Threads = 1024;             // K1 block: 16 waves over one kChunk
 struct K1Lds {
     static constexpr int k255 = 0;           // 256 doubles
     static constexpr int ent = 2048;         // 256 ClsEnt (16 B)
-    static constexpr int sthr = 6144;        // 256 x uint4 saturation-class thresholds
-    static constexpr int red = 10240;        // 16 waves x 8 x u64
-    static constexpr int qn = 11264;         // 2 ints (+pad)
-    static constexpr int queue = 11280;      // kQueue x u16 (pixel offset in the chunk)
-    static constexpr int hist = queue + 2 * kQueue;   // K1: 2 x (tl+1) x C lane copies + tl; K3: rules, sums
+    static constexpr int red = 6144;         // 16 waves x 8 x u64
+    static constexpr int qn = 7168;          // Kcut scratch (16 B)
+    static constexpr int area = 7184;        // K1: 2 x (tl+1) x C chunk-count copies + tl; K3: rules, sums
 };
 static_assert(sizeof(ClsEnt) == 16, "ClsEnt is one 16-B LDS read");
 
@@ -39,7 +36,6 @@ __device__ __forceinline__ void stage_tables(unsigned char* smem, const double* 
     for (int i = tid; i < 256; i += blockDim.x) {
         reinterpret_cast<double*>(smem + K1Lds::k255)[i] = k255g[i];
         reinterpret_cast<ClsEnt*>(smem + K1Lds::ent)[i] = tabs->ent[i];
-        reinterpret_cast<uint4*>(smem + K1Lds::sthr)[i] = reinterpret_cast<const uint4*>(tabs->sthr)[i];
     }
 }
 
@@ -87,9 +83,8 @@ __device__ __forceinline__ void hist_add(unsigned* lds, int g) {
     }
 }
 
-#ifndef PHD_K1_ABLATE
-#define PHD_K1_ABLATE 0        // K1 ablation mask for timing builds (8 classify, 16 hist, 32 sat, 128 atomics)
-#endif
+// ablate (PHD_ABLATE, timing runs only): K1 8 classify, 16 hist atomic, 32 sat,
+// 64 chunk fold, 128 global atomics; K3 8 classify, 16 LDS sums, 32 hue
 #ifndef PHD_K1_MINWAVES
 #define PHD_K1_MINWAVES 8        // waves/SIMD the statistics-only K1 is sized for (2 blocks/CU)
 #endif
@@ -143,8 +138,9 @@ __device__ __forceinline__ void load_group(const uint8_t* ip, long p0, bool ok, 
 // an image.  The per-chunk group counts are built in LDS (double-buffered, so
 // a chunk costs two barriers), written out for the cutoff search, and summed
 // into a per-run LDS histogram that is flushed with the moments.  Pixels
-// classify through classify(); the few near a bin edge are queued and
-// classified exactly after the chunk's stream so waves stay convergent.  The
+// classify through classify_e() (branch-free, four pixels' table reads in
+// flight); the few whose hue lies exactly on a bin edge are marked in a
+// per-thread mask and classified exactly after the chunk's stream.  The
 // next item's loads are issued before the current chunk's barriers.
 // The chunk counts have C = 1 << cshift lane-private copies (lane l adds to
 // copy l mod C), so the per-pixel LDS atomics never collide within a wave.
@@ -155,24 +151,21 @@ __device__ __forceinline__ void load_group(const uint8_t* ip, long p0, bool ok, 
 // image end are masked to (0, 0, 0) pixels, which add nothing to the moments
 // or sum(s) and are taken back out of the histogram; the < 4 pixels of a
 // partial final group are done by one thread of the last chunk.
-template <bool kHist, bool kAligned>
+template <bool kHist, bool kAligned, bool kThr>
 __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_MINWAVES) void k_hsv_stats(
         const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
         const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, PaletteDev out, long a_stride,
-        long h_stride, int cshift) {
-    constexpr int ablate = PHD_K1_ABLATE;   // compile-time ablation (timing builds only)
+        long h_stride, int cshift, int ablate_arg) {
+    const int ablate = PHD_ABL(ablate_arg);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
     const signed char* si8 = tabs->si8;                                 // global (s_partitions > 8 only)
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + K1Lds::red);
-    int* qn = reinterpret_cast<int*>(smem + K1Lds::qn);
-    unsigned short* queue = reinterpret_cast<unsigned short*>(smem + K1Lds::queue);
     const int tl = gp.tl;
     const int tl1 = tl + 1;                                             // + dummy slot (deferred pixels)
     const int C = 1 << cshift, cm = C - 1;
-    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);   // [2][tl1][C] chunk counts
+    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::area);   // [2][tl1][C] chunk counts
     unsigned* seg = lh + 2 * tl1 * C;                                  // [tl] counts of the run
     const int tid = threadIdx.x;
     const int mycopy = tid & cm;
@@ -181,7 +174,6 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
     stage_tables(smem, k255g, tabs);
     if (kHist) {
         for (int i = tid; i < 2 * tl1 * C + tl; i += kK1Threads) lh[i] = 0;
-        if (tid < 2) qn[tid] = 0;
     }
     __syncthreads();
 
@@ -215,27 +207,33 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
         // one group (4 pixels) per iteration; the words rotate through
         // registers so the loop is not unrolled (bounded live state)
         unsigned bits = okb;
+        unsigned emask = 0;                                  // this thread's edge pixels (bit 4*st + i)
         unsigned c0 = (bits & 1) ? w[0][0] : 0u, c1 = (bits & 1) ? w[0][1] : 0u, c2 = (bits & 1) ? w[0][2] : 0u;
 #pragma unroll 1
         for (int st = 0; st < kSteps; st++) {
-            const int o0 = 4 * tid + 4 * kK1Threads * st;     // offset in the chunk
             const unsigned cw[3] = {c0, c1, c2};
+            // phase 1: bytes, moments, the 4 table reads; phase 2: groups
+            int kr[4], kg[4], kb[4];
+            ClsEnt e[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int kr = px_byte(cw, 3 * i), kg = px_byte(cw, 3 * i + 1), kb = px_byte(cw, 3 * i + 2);
-                sr += kr; sg += kg; sb += kb;
-                qr += kr * kr; qg += kg * kg; qb += kb * kb;
+                kr[i] = px_byte(cw, 3 * i);
+                kg[i] = px_byte(cw, 3 * i + 1);
+                kb[i] = px_byte(cw, 3 * i + 2);
+                sr += kr[i]; sg += kg[i]; sb += kb[i];
+                qr += kr[i] * kr[i]; qg += kg[i] * kg[i]; qb += kb[i] * kb[i];
+                if (kHist) e[i] = ent[max(kr[i], max(kg[i], kb[i]))];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int kmx = max(kr[i], max(kg[i], kb[i])), kmn = min(kr[i], min(kg[i], kb[i]));
+                if (!(ablate & 32)) ssum += sat_of(kmx, kmn);
                 if (kHist) {
-                    double sv = 0.0;
-                    int g = (ablate & 8) ? (kr & 63) : classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
-                    if (!(ablate & 32)) ssum += sv;
-                    if (g == -2) {            // on a hue bin edge: classify exactly after the stream
-                        queue[atomicAdd(&qn[par], 1)] = (unsigned short)(o0 + i);
-                        g = tl;
-                    }
-                    if (!(ablate & 16)) atomicAdd(&ch[(g << cshift) | mycopy], 1u);
-                } else {
-                    if (!(ablate & 32)) ssum += sat_only(kr, kg, kb, ent);
+                    const int g = (ablate & 8) ? (kr[i] % tl) : classify_e<kThr>(kr[i], kg[i], kb[i], e[i], si8, gp, fc);
+                    // a hue exactly on a bin edge (g == -2): counted after the stream
+                    const int edge = g == -2;
+                    emask |= (unsigned)edge << (4 * st + i);
+                    if (!(ablate & 16)) atomicAdd(&ch[((edge ? tl : g) << cshift) | mycopy], 1u);
                 }
             }
             bits >>= 1;
@@ -258,18 +256,25 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
                 qr += kr * kr; qg += kg * kg; qb += kb * kb;
                 double sv;
                 if (kHist) {
-                    int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
+                    int g = classify<kThr>(kr, kg, kb, ent, si8, gp, fc, sv);
                     if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
                     atomicAdd(&ch[g << cshift], 1u);
                 } else {
-                    sv = sat_only(kr, kg, kb, ent);
+                    sv = sat_only(kr, kg, kb);
                 }
                 ssum += sv;
             }
         }
+        // this thread's edge pixels: the exact group (fp64 hue, rgb2hsv's order)
+        while (kHist && emask) {
+            const int bt = __ffs(emask) - 1;
+            emask &= emask - 1;
+            const long p = base + 4L * tid + 4L * kK1Threads * (bt >> 2) + (bt & 3);
+            const int g = exact_group(ip[3 * p], ip[3 * p + 1], ip[3 * p + 2], k255, gp);
+            atomicAdd(&ch[(g << cshift) | mycopy], 1u);
+        }
         // next work item: prefetch its pixels now
         const int cimg = img, cc = c;
-        const uint8_t* cip = ip;
         if (++c == nchunks) {
             c = 0;
             img++;
@@ -280,23 +285,16 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
             issue(ip, c);
         }
         if (kHist) {
-            __syncthreads();
             // zero pixels of masked groups (a whole-group count per chunk)
             const long pad = base + kChunk - full_end;
             if (pad > 0 && tid == 0) {
                 double sv;
-                atomicSub(&ch[classify(0, 0, 0, ent, sthr, si8, gp, fc, sv) << cshift], (unsigned)pad);
-            }
-            const int nq = qn[par];
-            for (int q = tid; q < nq; q += kK1Threads) {
-                const long p = base + queue[q];
-                atomicAdd(&ch[(exact_group(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp) << cshift) | mycopy],
-                          1u);
+                atomicSub(&ch[classify<kThr>(0, 0, 0, ent, si8, gp, fc, sv) << cshift], (unsigned)pad);
             }
             __syncthreads();
             // fold the C copies of each group (C consecutive lanes) with shuffles
             unsigned short* chunk_out = img_chunks(out, h_stride, cimg) + (long)cc * tl;
-            const int ncopy = tl << cshift;
+            const int ncopy = (ablate & 64) ? 0 : tl << cshift;
             for (int i0 = tid; i0 < ((ncopy + kK1Threads - 1) & ~(kK1Threads - 1)); i0 += kK1Threads) {
                 unsigned n = 0;
                 if (i0 < ncopy) {
@@ -310,8 +308,7 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
                     seg[g] += n;
                 }
             }
-            if (tid < C) ch[(tl << cshift) + tid] = 0;        // the deferred-pixel slot
-            if (tid == 0) qn[par] = 0;
+            if (tid < C) ch[(tl << cshift) + tid] = 0;        // the edge-pixel slot
         }
         if (!more || img != cimg || it + 1 - seg_it0 == 4096) {
             // the run leaves image cimg (or its u32 moments could overflow):
@@ -398,11 +395,11 @@ __device__ unsigned long long block_excl_scan_k1_u64(unsigned long long x, unsig
 }
 
 // Exact group of a pixel: classify(), and the exact hue on a bin edge.
-__device__ __forceinline__ int exact_group_t(int kr, int kg, int kb, const ClsEnt* ent, const uint4* sthr,
-                                             const signed char* si8, const double* k255, const GridParams& gp,
+template <bool kThr>
+__device__ __forceinline__ int exact_group_t(int kr, int kg, int kb, const ClsEnt* ent, const signed char* si8, const double* k255, const GridParams& gp,
                                              const FastCls& fc, double& s) {
-    int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, s);
-    if (g == -2) g = edge_group(kr, kg, kb, hue_exact(kr, kg, kb, k255), ent, sthr, si8, gp, fc);
+    int g = classify<kThr>(kr, kg, kb, ent, si8, gp, fc, s);
+    if (g == -2) g = edge_group<kThr>(kr, kg, kb, hue_exact(kr, kg, kb, k255), ent, si8, gp);
     return g;
 }
 
@@ -413,7 +410,7 @@ __device__ __forceinline__ int exact_group_t(int kr, int kg, int kb, const ClsEn
 // keep-th pixel (cutoff = index + 1) and of its last pixel (the dangling
 // node).  The per-chunk counts of K1 locate the chunk; one pass over that
 // chunk's 16384 pixels (16 per thread) and a block scan find the pixel.
-template <bool kAligned>
+template <bool kAligned, bool kThr>
 __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
         const uint8_t* const* __restrict__ imgs, long npix, int nchunks, GridParams gp, FastCls fc,
         const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, const int2* __restrict__ entries,
@@ -421,7 +418,6 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
     const signed char* si8 = tabs->si8;
     int* scratch = reinterpret_cast<int*>(smem + K1Lds::red);          // 16 x u64
     int* misc = reinterpret_cast<int*>(smem + K1Lds::red + 256);       // chunk, rank, last chunk
@@ -478,7 +474,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
                     continue;
                 }
                 double sv;
-                if (exact_group_t(kr, kg, kb, ent, sthr, si8, k255, gp, fc, sv) == g) hits |= 1u << (4 * st + i);
+                if (exact_group_t<kThr>(kr, kg, kb, ent, si8, k255, gp, fc, sv) == g) hits |= 1u << (4 * st + i);
             }
         }
         if (tid == 0) *found = 0;
@@ -529,31 +525,39 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
 // the fp64 LDS atomics of one wave hit distinct addresses (and, for C = 32,
 // distinct banks), whatever the image.  Per image, the copies are folded and
 // go to HBM with one atomic per slot and field.
-template <bool kAligned>
+template <bool kAligned, bool kThr>
 __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
         const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
         const ClassTables* __restrict__ tabs, const double* __restrict__ k255g,
         const GroupRule* __restrict__ rules0, const double* __restrict__ off0, long b_stride,
-        const int* __restrict__ nslots_img, int max_slots, double* out0, long c_stride, int cshift) {
+        const int* __restrict__ nslots_img, int max_slots, double* out0, long c_stride, int cshift,
+        int ablate_arg) {
+    const int ablate = PHD_ABL(ablate_arg);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
     const signed char* si8 = tabs->si8;
     const int tl = gp.tl;
     const int C = 1 << cshift, cm = C - 1;
-    uint4* rec = reinterpret_cast<uint4*>(smem + K1Lds::queue);        // [tl] {slot, cut, last, -}
-    double* off = reinterpret_cast<double*>(rec + tl);                 // [max_slots]
-    double* acc = off + max_slots;                                     // [3][max_slots][C] h, s, v
-    unsigned* cnt = reinterpret_cast<unsigned*>(acc + 3 * max_slots * C);   // [max_slots][C]
+    // slot ms = max_slots and rule tl are dummies: pixels that are not kept
+    // add into them, so the per-pixel code has no branch
+    const int ms = max_slots + 1;
+    uint4* rec = reinterpret_cast<uint4*>(smem + K1Lds::area);        // [tl + 1] {slot, cut, last, -}
+    double* off = reinterpret_cast<double*>(rec + tl + 1);             // [ms]
+    double* acc = off + ms;                                            // [3][ms][C] h, s, v
+    unsigned* cnt = reinterpret_cast<unsigned*>(acc + 3 * ms * C);     // [ms][C]
     const int tid = threadIdx.x;
     const int mycopy = tid & cm;
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
     stage_tables(smem, k255g, tabs);
-    for (int i = tid; i < max_slots * C; i += kK1Threads) {
-        acc[i] = acc[max_slots * C + i] = acc[2 * max_slots * C + i] = 0.0;
+    for (int i = tid; i < ms * C; i += kK1Threads) {
+        acc[i] = acc[ms * C + i] = acc[2 * ms * C + i] = 0.0;
         cnt[i] = 0;
+    }
+    if (tid == 0) {
+        rec[tl] = make_uint4(0xFFFFFFFFu, 0u, 0xFFFFFFFFu, 0u);
+        off[max_slots] = 0.0;
     }
 
     constexpr int kSteps = kChunk / (4 * kK1Threads);
@@ -576,6 +580,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                 rec[i] = q;
             }
             for (int i = tid; i < ns; i += kK1Threads) off[i] = offi[i];
+            for (int i = ns + tid; i < max_slots; i += kK1Threads) off[i] = 0.0;
             cur = img;
             __syncthreads();
         }
@@ -587,6 +592,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
             const long p0 = base + 4L * tid + 4L * kK1Threads * st;
             load_group<kAligned>(ip, p0, p0 < full_end, w[st]);
         }
+        unsigned emask = 0;                                  // this thread's edge pixels (bit 4*st + i)
 #pragma unroll 1
         for (int st = 0; st < kSteps; st++) {
             const long p0 = base + 4L * tid + 4L * kK1Threads * st;
@@ -595,41 +601,71 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
 #pragma unroll
             for (int k = 0; k < kSteps; k++)
                 if (k == st) { cw[0] = w[k][0]; cw[1] = w[k][1]; cw[2] = w[k][2]; }
+            // phases over the 4 pixels, so each step has 4 independent LDS reads
+            // in flight: class entry -> group -> keep rule -> slot offset
+            int kr[4], kg[4], kb[4], sl[4];
+            ClsEnt e[4];
+            uint4 q[4];
+            double o[4];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int kr = px_byte(cw, 3 * i), kg = px_byte(cw, 3 * i + 1), kb = px_byte(cw, 3 * i + 2);
-                double sv;
-                int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
-                const uint4 q = rec[g == -2 ? 0 : g];
+                kr[i] = px_byte(cw, 3 * i);
+                kg[i] = px_byte(cw, 3 * i + 1);
+                kb[i] = px_byte(cw, 3 * i + 2);
+                e[i] = ent[max(kr[i], max(kg[i], kb[i]))];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int g = (ablate & 8) ? (kr[i] % tl) : classify_e<kThr>(kr[i], kg[i], kb[i], e[i], si8, gp, fc);
+                const int edge = g == -2;                    // exact group after the stream
+                emask |= (unsigned)(edge & (int)okg) << (4 * st + i);
+                q[i] = rec[edge ? tl : g];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
                 const unsigned idx = (unsigned)(p0 + i);
-                bool kept = okg && (int)q.x >= 0 && (idx < q.y || idx == q.z);
-                if (g == -2 || kept) {
-                    const double hx = hue_exact(kr, kg, kb, k255);
-                    if (g == -2) {                           // on a hue bin edge: the exact group
-                        g = edge_group(kr, kg, kb, hx, ent, sthr, si8, gp, fc);
-                        const uint4 r = rec[g];
-                        kept = okg && (int)r.x >= 0 && (idx < r.y || idx == r.z);
-                        if (kept) {
-                            const int sl = (int)r.x;
-                            double tp = hx + off[sl];
-                            tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
-                            const int a = (sl << cshift) | mycopy;
-                            atomicAdd(&acc[a], tp);
-                            atomicAdd(&acc[max_slots * C + a], sv);
-                            atomicAdd(&acc[2 * max_slots * C + a], v_of(max(kr, max(kg, kb)), k255));
-                            atomicAdd(&cnt[a], 1u);
-                        }
-                    } else {
-                        const int sl = (int)q.x;
-                        double tp = hx + off[sl];
-                        tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
-                        const int a = (sl << cshift) | mycopy;
-                        atomicAdd(&acc[a], tp);
-                        atomicAdd(&acc[max_slots * C + a], sv);
-                        atomicAdd(&acc[2 * max_slots * C + a], v_of(max(kr, max(kg, kb)), k255));
-                        atomicAdd(&cnt[a], 1u);
-                    }
+                const bool kept = okg && (int)q[i].x >= 0 && (idx < q[i].y || idx == q[i].z);
+                sl[i] = kept ? (int)q[i].x : max_slots;
+                o[i] = off[sl[i]];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                // wrap(h + off) (calculate_avg_hsv, src/color_quantization.c:536-540): h from a
+                // reciprocal (within an ulp); the exact quotient decides the wrap whenever
+                // h + off is within 1e-9 of 0 or 360
+                const int kmx = max(kr[i], max(kg[i], kb[i])), kmn = min(kr[i], min(kg[i], kb[i]));
+                double tp = ((ablate & 32) ? 0.0 : hue_fast(kr[i], kg[i], kb[i])) + o[i];
+                if (fabs(tp - 360.0) < 1e-9 || fabs(tp) < 1e-9) tp = hue_exact(kr[i], kg[i], kb[i], k255) + o[i];
+                tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+                const int a = (sl[i] << cshift) | mycopy;
+                if (!(ablate & 16)) {
+                    atomicAdd(&acc[a], tp);
+                    atomicAdd(&acc[ms * C + a], sat_of(kmx, kmn));
+                    atomicAdd(&acc[2 * ms * C + a], v_fast(kmx));
+                    atomicAdd(&cnt[a], 1u);
                 }
+            }
+        }
+        // this thread's edge pixels: exact hue and group (rgb2hsv's order)
+        while (emask) {
+            const int bt = __ffs(emask) - 1;
+            emask &= emask - 1;
+            const long p = base + 4L * tid + 4L * kK1Threads * (bt >> 2) + (bt & 3);
+            const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
+            const double hx = hue_exact(kr, kg, kb, k255);
+            const int g = edge_group<kThr>(kr, kg, kb, hx, ent, si8, gp);
+            const uint4 r = rec[g];
+            const unsigned idx = (unsigned)p;
+            if ((int)r.x >= 0 && (idx < r.y || idx == r.z)) {
+                const int sl = (int)r.x;
+                double tp = hx + off[sl];
+                tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+                const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
+                const int a = (sl << cshift) | mycopy;
+                atomicAdd(&acc[a], tp);
+                atomicAdd(&acc[ms * C + a], sat_of(kmx, kmn));
+                atomicAdd(&acc[2 * ms * C + a], v_fast(kmx));
+                atomicAdd(&cnt[a], 1u);
             }
         }
         if (base + kChunk >= npix && tid == 0) {
@@ -638,8 +674,8 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                 const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
                 double sv;
                 const double hx = hue_exact(kr, kg, kb, k255);
-                int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
-                if (g == -2) g = edge_group(kr, kg, kb, hx, ent, sthr, si8, gp, fc);
+                int g = classify<kThr>(kr, kg, kb, ent, si8, gp, fc, sv);
+                if (g == -2) g = edge_group<kThr>(kr, kg, kb, hx, ent, si8, gp);
                 const uint4 q = rec[g];
                 const unsigned idx = (unsigned)p;
                 if ((int)q.x >= 0 && (idx < q.y || idx == q.z)) {
@@ -648,8 +684,8 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                     tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
                     const int a = sl << cshift;
                     atomicAdd(&acc[a], tp);
-                    atomicAdd(&acc[max_slots * C + a], sv);
-                    atomicAdd(&acc[2 * max_slots * C + a], v_of(max(kr, max(kg, kb)), k255));
+                    atomicAdd(&acc[ms * C + a], sv);
+                    atomicAdd(&acc[2 * ms * C + a], v_of(max(kr, max(kg, kb)), k255));
                     atomicAdd(&cnt[a], 1u);
                 }
             }
@@ -671,7 +707,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                 double a = 0.0;
                 if (i0 < total) {
                     if (f < 3) {
-                        double* src = &acc[f * max_slots * C + j];
+                        double* src = &acc[f * ms * C + j];
                         a = *src;
                         *src = 0.0;
                     } else {
@@ -688,6 +724,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
 }
 
 // K1 for downsample_rate > 1: HSV over the decimated pixels only (gathered).
+template <bool kThr>
 __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__ img, long npix,
                                                      int width, int ds, int nw, GridParams gp, FastCls fc,
                                                      const ClassTables* __restrict__ tabs,
@@ -695,10 +732,9 @@ __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
     const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
-    const uint4* sthr = reinterpret_cast<const uint4*>(smem + K1Lds::sthr);
     const signed char* si8 = tabs->si8;
     double* red = reinterpret_cast<double*>(smem + K1Lds::red);
-    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::hist);
+    unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::area);
     const int tid = threadIdx.x;
     stage_tables(smem, k255g, tabs);
     for (int i = tid; i < gp.tl; i += kThreads) lh[i] = 0;
@@ -710,7 +746,7 @@ __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__
         const long p = src_pixel(j, width, ds, nw);
         const int kr = img[3 * p], kg = img[3 * p + 1], kb = img[3 * p + 2];
         double sv;
-        int g = classify(kr, kg, kb, ent, sthr, si8, gp, fc, sv);
+        int g = classify<kThr>(kr, kg, kb, ent, si8, gp, fc, sv);
         ssum += sv;
         if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
         hist_add(lh, g);
@@ -941,13 +977,14 @@ __global__ __launch_bounds__(kThreads) void k_palette_sums(const uint8_t* __rest
 
 // Per-pixel group id through the production classifier (classify, exact
 // fallback) and exact HSV: validation of the device arithmetic.
+template <bool kThr>
 __global__ void k_debug_hsv(const uint8_t* __restrict__ img, long n, GridParams gp, FastCls fc,
                             const ClassTables* __restrict__ tabs, const double* __restrict__ k255,
                             int* __restrict__ gid, double* __restrict__ hsv) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const int kr = img[3 * i], kg = img[3 * i + 1], kb = img[3 * i + 2];
         double sv;
-        int g = classify(kr, kg, kb, tabs->ent, reinterpret_cast<const uint4*>(tabs->sthr), tabs->si8, gp, fc, sv);
+        int g = classify<kThr>(kr, kg, kb, tabs->ent, tabs->si8, gp, fc, sv);
         if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
         gid[i] = g;
         if (hsv) {
@@ -997,6 +1034,11 @@ static inline long hsv_pixels(int height, int width, int ds, int* nw) {
     return (long)(short)hh * (short)ww;   // rgb2hsv's short dimensions, image_processing.c:378-383
 }
 
+int env_ablate() {
+    static const int a = getenv("PHD_ABLATE") ? atoi(getenv("PHD_ABLATE")) : 0;   // timing runs only
+    return a;
+}
+
 // lane-private copies of K1's chunk counts: as many as fit 40 KiB (<= 32)
 int k1_cshift(int tl) {
     int c = 5;
@@ -1007,12 +1049,12 @@ int k1_cshift(int tl) {
 // ... and of K3's slot sums (28 B per copy): <= 96 KiB
 int k3_cshift(int max_slots) {
     int c = 5;
-    while (c > 0 && (size_t)max_slots * (28u << c) > 96 * 1024) c--;
+    while (c > 0 && ((size_t)max_slots + 1) * (28u << c) > 96 * 1024) c--;
     return c;
 }
 
 size_t hsv_stats_lds(const GridParams& gp, bool hist) {
-    return hist ? K1Lds::hist + sizeof(unsigned) * (2 * ((size_t)gp.tl + 1) * (1u << k1_cshift(gp.tl)) + gp.tl)
+    return hist ? K1Lds::area + sizeof(unsigned) * (2 * ((size_t)gp.tl + 1) * (1u << k1_cshift(gp.tl)) + gp.tl)
                 : (size_t)K1Lds::red + 1024;
 }
 
@@ -1025,23 +1067,28 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     const size_t lds = hsv_stats_lds(gp, hist);
     const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
-#define PHD_K1_LAUNCH(H, A)                                                                                   \
+#define PHD_K1_LAUNCH(H, A, T)                                                                                   \
     do {                                                                                                      \
         static bool attr = false;                                                                             \
         if (!attr) {                                                                                          \
-            (void)hipFuncSetAttribute((const void*)k_hsv_stats<H, A>,                                         \
+            (void)hipFuncSetAttribute((const void*)k_hsv_stats<H, A, T>,                                      \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                \
             attr = true;                                                                                      \
         }                                                                                                     \
-        hipLaunchKernelGGL((k_hsv_stats<H, A>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix, nchunks, \
-                           nitems, gp, fc, tabs, k255, out0, a_stride, h_stride, k1_cshift(gp.tl));           \
+        hipLaunchKernelGGL((k_hsv_stats<H, A, T>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix, nchunks, \
+                           nitems, gp, fc, tabs, k255, out0, a_stride, h_stride, k1_cshift(gp.tl), env_ablate()); \
     } while (0)
     if (hist) {
-        if (aligned) PHD_K1_LAUNCH(true, true);
-        else PHD_K1_LAUNCH(true, false);
-    } else {
-        if (aligned) PHD_K1_LAUNCH(false, true);
-        else PHD_K1_LAUNCH(false, false);
+        if (fc.use_thr) {
+            if (aligned) PHD_K1_LAUNCH(true, true, true);
+            else PHD_K1_LAUNCH(true, false, true);
+        } else {
+            if (aligned) PHD_K1_LAUNCH(true, true, false);
+            else PHD_K1_LAUNCH(true, false, false);
+        }
+    } else {   // the statistics pass does not classify
+        if (aligned) PHD_K1_LAUNCH(false, true, true);
+        else PHD_K1_LAUNCH(false, false, true);
     }
 #undef PHD_K1_LAUNCH
     return hipGetLastError();
@@ -1052,14 +1099,13 @@ hipError_t launch_hsv_ds(const uint8_t* img, int height, int width, int ds, cons
                          const double* k255, hipStream_t st) {
     int nw;
     const long n = hsv_pixels(height, width, ds, &nw);
-    const size_t lds = K1Lds::hist + sizeof(unsigned) * ((gp.tl + 3) & ~3);
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_hsv_ds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
-    hipLaunchKernelGGL(k_hsv_ds, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc, tabs,
-                       k255, out);
+    const size_t lds = K1Lds::area + sizeof(unsigned) * ((gp.tl + 3) & ~3);
+    if (fc.use_thr)
+        hipLaunchKernelGGL(k_hsv_ds<true>, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
+                           tabs, k255, out);
+    else
+        hipLaunchKernelGGL(k_hsv_ds<false>, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
+                           tabs, k255, out);
     const long nbytes = 3L * height * width;
     const int blocks = (int)std::min<long>(2048, (nbytes / 3 + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_stats, dim3(blocks), dim3(kThreads), 0, st, img, nbytes, out.sums);
@@ -1092,7 +1138,8 @@ hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds
 }
 
 size_t palette_sums_b_lds(int tl, int max_slots) {
-    return (size_t)K1Lds::queue + 16 * (size_t)tl + 8 * (size_t)max_slots + (size_t)max_slots * (28u << k3_cshift(max_slots));
+    return (size_t)K1Lds::area + 16 * ((size_t)tl + 1) + 8 * ((size_t)max_slots + 1) +
+           ((size_t)max_slots + 1) * (28u << k3_cshift(max_slots));
 }
 
 hipError_t launch_cutoffs_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n, int height,
@@ -1105,20 +1152,25 @@ hipError_t launch_cutoffs_batch(const uint8_t* const* d_imgs, const uint8_t* con
     const int nchunks = (int)((npix + kChunk - 1) / kChunk);
     bool aligned = true;
     for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
-    const size_t lds = K1Lds::queue;
-#define PHD_KCUT_LAUNCH(A)                                                                                  \
+    const size_t lds = K1Lds::area;
+#define PHD_KCUT_LAUNCH(A, T)                                                                               \
     do {                                                                                                    \
         static bool attr = false;                                                                           \
         if (!attr) {                                                                                        \
-            (void)hipFuncSetAttribute((const void*)k_cutoffs_b<A>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+            (void)hipFuncSetAttribute((const void*)k_cutoffs_b<A, T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                       160 * 1024);                                                          \
             attr = true;                                                                                    \
         }                                                                                                   \
-        hipLaunchKernelGGL((k_cutoffs_b<A>), dim3(n_entries), dim3(kK1Threads), lds, st, d_imgs, npix,        \
+        hipLaunchKernelGGL((k_cutoffs_b<A, T>), dim3(n_entries), dim3(kK1Threads), lds, st, d_imgs, npix,        \
                            nchunks, gp, fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, b_stride);  \
     } while (0)
-    if (aligned) PHD_KCUT_LAUNCH(true);
-    else PHD_KCUT_LAUNCH(false);
+    if (fc.use_thr) {
+        if (aligned) PHD_KCUT_LAUNCH(true, true);
+        else PHD_KCUT_LAUNCH(false, true);
+    } else {
+        if (aligned) PHD_KCUT_LAUNCH(true, false);
+        else PHD_KCUT_LAUNCH(false, false);
+    }
 #undef PHD_KCUT_LAUNCH
     return hipGetLastError();
 }
@@ -1135,27 +1187,35 @@ hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
     const size_t lds = palette_sums_b_lds(gp.tl, max_slots);
     const int grid = (int)std::min<long>(nitems, num_cus());
-#define PHD_K3_LAUNCH(A)                                                                                    \
+#define PHD_K3_LAUNCH(A, T)                                                                                 \
     do {                                                                                                    \
         static bool attr = false;                                                                           \
         if (!attr) {                                                                                        \
-            (void)hipFuncSetAttribute((const void*)k_palette_sums_b<A>,                                     \
+            (void)hipFuncSetAttribute((const void*)k_palette_sums_b<A, T>,                                  \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              \
             attr = true;                                                                                    \
         }                                                                                                   \
-        hipLaunchKernelGGL((k_palette_sums_b<A>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix,        \
+        hipLaunchKernelGGL((k_palette_sums_b<A, T>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix,        \
                            nchunks, nitems, gp, fc, tabs, k255, rules0, off0, b_stride, nslots_img,         \
-                           max_slots, out0, c_stride, k3_cshift(max_slots));                                \
+                           max_slots, out0, c_stride, k3_cshift(max_slots), env_ablate());                  \
     } while (0)
-    if (aligned) PHD_K3_LAUNCH(true);
-    else PHD_K3_LAUNCH(false);
+    if (fc.use_thr) {
+        if (aligned) PHD_K3_LAUNCH(true, true);
+        else PHD_K3_LAUNCH(false, true);
+    } else {
+        if (aligned) PHD_K3_LAUNCH(true, false);
+        else PHD_K3_LAUNCH(false, false);
+    }
 #undef PHD_K3_LAUNCH
     return hipGetLastError();
 }
 
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st) {
-    hipLaunchKernelGGL(k_debug_hsv, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
+    if (fc.use_thr)
+        hipLaunchKernelGGL(k_debug_hsv<true>, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
+    else
+        hipLaunchKernelGGL(k_debug_hsv<false>, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
     return hipGetLastError();
 }
 

@@ -8,6 +8,14 @@
 
 #include <hip/hip_runtime.h>
 
+// Ablation switches for timing experiments exist only in builds made with
+// -DPHD_ABLATE_BUILD (a separate library, tools/); in the product they are 0.
+#ifdef PHD_ABLATE_BUILD
+#define PHD_ABL(x) (x)
+#else
+#define PHD_ABL(x) 0
+#endif
+
 #include <algorithm>
 
 #include "phd_internal.h"
@@ -55,29 +63,44 @@ __device__ __forceinline__ int group_of(const GridParams& gp, double h, double s
 // gap to any integer and truncates to floor(N/D) exactly.  When D divides N
 // and num is not 0 or +-d, the reference's double hue may round either side
 // of the edge: those pixels (-2) take the fp64 path.  Select-only code.
+// 1 / k for k in [1, 255] to within an ulp (v_rcp_f64 + one Newton step).
+__device__ __forceinline__ double inv_k(int k) {
+    const double d = (double)k;
+    const double r = __builtin_amdgcn_rcp(d);
+    return fma(fma(-d, r, 1.0), r, r);
+}
+
+// rgb2hsv's s (src/image_processing.c:408-414) to within an ulp: 0 for d == 0,
+// 0.999999 for d == max, else d / max.  Feeds only sums (S-bar, palette).
+__device__ __forceinline__ double sat_of(int kmx, int kmn) {
+    const int kd = kmx - kmn;
+    const double s = (double)kd * inv_k(max(kmx, 1));
+    return kd == 0 ? 0.0 : (kmn == 0 ? 0.999999 : s);
+}
+
 // Si of arm_octree (src/color_quantization.c:140) for (kmax, kd): the threshold
-// count of ClassTables::sthr (LDS copy), or the full table in global memory.
-__device__ __forceinline__ int si_of(int kmx, int kd, const uint4* sthr, const signed char* si8g,
-                                     const FastCls& F) {
-    if (F.use_thr) {
-        const uint4 t = sthr[kmx];
+// count of the pixel's ClsEnt (kThr: FastCls::use_thr), or the full table in
+// global memory.  Kernels are instantiated for both, so the per-pixel code has
+// no branch and no global load on the threshold path.
+template <bool kThr>
+__device__ __forceinline__ int si_of(const ClsEnt& e, int kmx, int kd, const signed char* si8g) {
+    if constexpr (kThr) {
         const unsigned u = (unsigned)kd;
-        return -1 + (int)(u >= (t.x & 0xFFFFu)) + (int)(u >= (t.x >> 16)) + (int)(u >= (t.y & 0xFFFFu)) +
-               (int)(u >= (t.y >> 16)) + (int)(u >= (t.z & 0xFFFFu)) + (int)(u >= (t.z >> 16)) +
-               (int)(u >= (t.w & 0xFFFFu)) + (int)(u >= (t.w >> 16));
+        return -1 + (int)(u >= (e.thr[0] & 0xFFFFu)) + (int)(u >= (e.thr[0] >> 16)) +
+               (int)(u >= (e.thr[1] & 0xFFFFu)) + (int)(u >= (e.thr[1] >> 16)) +
+               (int)(u >= (e.thr[2] & 0xFFFFu)) + (int)(u >= (e.thr[2] >> 16));
     }
     return si8g[(kmx << 8) | kd];
 }
 
-__device__ __forceinline__ int classify(int kr, int kg, int kb, const ClsEnt* ent, const uint4* sthr,
-                                        const signed char* si8g, const GridParams& gp, const FastCls& F,
-                                        double& s_out) {
+// classify() from the pixel's table entry (ent[max channel], read by the
+// caller so that several pixels' LDS reads are in flight together).
+// Branch-free: bitwise ands and selects only.
+template <bool kThr>
+__device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& e, const signed char* si8g,
+                                          const GridParams& gp, const FastCls& F) {
     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
-    const ClsEnt e = ent[kmx];
-    // s exactly as rgb2hsv up to the last ulp: 0 (d == 0), 0.999999 (d == max), else d / max
-    const double s = (double)kd * e.rinv;
-    s_out = (kmn == 0 && kd != 0) ? 0.999999 : s;
-    const int si = si_of(kmx, kd, sthr, si8g, F);
+    const int si = si_of<kThr>(e, kmx, kd, si8g);
     // hue bin
     const bool isr = kr == kmx, isg = kg == kmx;
     const int a = isr ? kg : (isg ? kb : kr), b = isr ? kb : (isg ? kr : kg);
@@ -86,13 +109,21 @@ __device__ __forceinline__ int classify(int kr, int kg, int kb, const ClsEnt* en
     const int kd1 = max(kd, 1);
     const int N = __mul24(base, kd1) + 60 * num, D = __mul24(F.lh, kd1);
     const int hi = (int)(((float)N + 0.5f) * __builtin_amdgcn_rcpf((float)D));
-    const bool special = num == 0 || num == kd || num == -kd;
-    const bool edge = !special && __mul24(hi, D) == N;
+    const int special = (int)(num == 0) | (int)(num == kd) | (int)(num == -kd);
+    const int edge = (special ^ 1) & (int)(__mul24(hi, D) == N);
     const int vi = (e.vpack << 16) >> 16, gray = e.vpack >> 16;
     int g = __mul24(__mul24(hi, gp.sp) + si, gp.vp) + vi;
     g = edge ? -2 : g;
     g = si < 0 ? gray : g;
     return vi < 0 ? gp.tl - 1 : g;
+}
+
+template <bool kThr>
+__device__ __forceinline__ int classify(int kr, int kg, int kb, const ClsEnt* ent, const signed char* si8g,
+                                        const GridParams& gp, const FastCls& F, double& s_out) {
+    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
+    s_out = sat_of(kmx, kmn);
+    return classify_e<kThr>(kr, kg, kb, ent[kmx], si8g, gp, F);
 }
 
 // rgb2hsv's hue, bit-exact (same doubles, same operation order), select-only:
@@ -110,13 +141,30 @@ __device__ __forceinline__ double hue_exact(int kr, int kg, int kb, const double
     return h < 0 ? h + 360 : h;
 }
 
+// rgb2hsv's hue to within a few ulps (the quotient through inv_k): for sums.
+__device__ __forceinline__ double hue_fast(int kr, int kg, int kb) {
+    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
+    const bool isr = kr == kmx, isg = kg == kmx;
+    const int num = isr ? kg - kb : (isg ? kb - kr : kr - kg);
+    const double sector = isr ? 0.0 : (isg ? 2.0 : 4.0);
+    const double h = 60 * (sector + (double)num * inv_k(max(kd, 1)));
+    return kd == 0 ? 0.0 : (h < 0 ? h + 360 : h);
+}
+
+// rgb2hsv's v (k/255, 0.999999 for 255) to within an ulp: for sums.
+__device__ __forceinline__ double v_fast(int kmx) {
+    return kmx == 255 ? 0.999999 : (double)kmx * (1.0 / 255.0);
+}
+
 // The group of a pixel that classify() left on a hue bin edge (-2: a colour
 // pixel), from its exact hue: arm_octree's (int)(h / Lh).
-__device__ __forceinline__ int edge_group(int kr, int kg, int kb, double h, const ClsEnt* ent, const uint4* sthr,
-                                          const signed char* si8g, const GridParams& gp, const FastCls& F) {
+template <bool kThr>
+__device__ __forceinline__ int edge_group(int kr, int kg, int kb, double h, const ClsEnt* ent,
+                                          const signed char* si8g, const GridParams& gp) {
     const int kmx = max(kr, max(kg, kb)), kd = kmx - min(kr, min(kg, kb));
-    const int si = si_of(kmx, kd, sthr, si8g, F);
-    const int vi = (ent[kmx].vpack << 16) >> 16;
+    const ClsEnt e = ent[kmx];
+    const int si = si_of<kThr>(e, kmx, kd, si8g);
+    const int vi = (e.vpack << 16) >> 16;
     const int hi = (int)(h / gp.Lh);
     return (hi * gp.sp + si) * gp.vp + vi;
 }
@@ -125,10 +173,8 @@ __device__ __forceinline__ int edge_group(int kr, int kg, int kb, double h, cons
 __device__ __forceinline__ double v_of(int kmx, const double* k255) { return kmx == 255 ? 0.999999 : k255[kmx]; }
 
 // HSV saturation alone (rgb2hsv's s), for the statistics-only pass.
-__device__ __forceinline__ double sat_only(int kr, int kg, int kb, const ClsEnt* ent) {
-    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
-    double s = (double)kd * ent[kmx].rinv;   // d == 0 gives 0 (rinv[0] == 0 covers max == 0)
-    return kmn == 0 && kd != 0 ? 0.999999 : s;
+__device__ __forceinline__ double sat_only(int kr, int kg, int kb) {
+    return sat_of(max(kr, max(kg, kb)), min(kr, min(kg, kb)));
 }
 
 // The reference's exact group of a pixel (rgb2hsv in fp64 + arm_octree).

@@ -31,20 +31,19 @@ struct GridParams {
 // bin edge (where the reference's double rounding decides) take the fp64 path.
 struct FastCls {
     int lh;                    // Lh = 360 / h_partitions (integer division, :41)
-    int use_thr;               // Si from ClassTables::sthr (s_partitions <= 8), else si8 in global memory
+    int use_thr;               // Si from ClsEnt::thr (s_partitions <= 6), else si8 in global memory
 };
-struct ClsEnt {                // per max channel value k (16 B: one LDS read)
-    double rinv;               // 1 / k (k > 0; 0 for k == 0), saturation sums
+// Si is non-decreasing in kd = kmax - kmin for a fixed kmax (s = d / max is), so
+// it is -1 plus the number of thresholds kd reaches.
+constexpr int kSiThresholds = 6;
+struct ClsEnt {                // per max channel value k (16 B: one LDS read per pixel)
     int vpack;                 // low 16 bits (signed): Vi of v(k), -1 when v < black_thresh;
                                // high 16 bits: gray group id of v(k)
-    int pad;
+    unsigned thr[3];           // u16 j (low half of thr[j/2] for even j): the smallest kd with
+                               // Si >= j, 0xFFFF = never (j < kSiThresholds)
 };
-struct ClassTables {           // device copy; ent and sthr are staged into LDS by the kernels
+struct ClassTables {           // device copy; ent is staged into LDS by the kernels
     ClsEnt ent[256];
-    // Si is non-decreasing in kd = kmax - kmin for a fixed kmax, so it is -1 plus
-    // the number of thresholds kd reaches: sthr[kmax][j] packs the smallest kd
-    // with Si >= 2i and >= 2i+1 (low / high 16 bits; 0xFFFF = never).
-    unsigned sthr[256][4];
     signed char si8[256 * 256];   // [kmax][kmax - kmin]: Si of s, -1 when s < gray_thresh
 };
 

@@ -88,7 +88,6 @@ void make_class_tables(const GridParams& g, FastCls* fc, ClassTables* t) {
     for (int k = 0; k < 256; k++) {
         const double v = (k == 255) ? 0.999999 : (double)k / 255.0;
         ClsEnt& e = t->ent[k];
-        e.rinv = k ? 1.0 / (double)k : 0.0;
         int vcol = -1, vgray = 0;
         if (v >= g.bt) {
             vcol = (int)((v - g.bt) / g.Lv);
@@ -105,19 +104,20 @@ void make_class_tables(const GridParams& g, FastCls* fc, ClassTables* t) {
         }
     }
     fc->lh = 360 / g.hp;
-    // threshold form of si8 (see ClassTables::sthr); valid while Si is
-    // non-decreasing in kd and takes at most 8 non-negative values
-    bool mono = g.sp <= 8;
+    // threshold form of si8 (ClsEnt::thr); valid while Si is non-decreasing
+    // in kd and takes at most kSiThresholds non-negative values
+    bool mono = g.sp <= kSiThresholds;
     for (int k = 0; k < 256 && mono; k++) {
-        unsigned short thr[8];
-        for (int j = 0; j < 8; j++) thr[j] = 0xFFFF;
+        unsigned short thr[kSiThresholds];
+        for (int j = 0; j < kSiThresholds; j++) thr[j] = 0xFFFF;
         for (int kd = 0; kd <= k; kd++) {
             const int si = t->si8[k * 256 + kd];
             if (kd > 0 && si < t->si8[k * 256 + kd - 1]) mono = false;
-            for (int j = 0; j <= si && j < 8; j++)
+            for (int j = 0; j <= si && j < kSiThresholds; j++)
                 if (thr[j] == 0xFFFF) thr[j] = (unsigned short)kd;
         }
-        for (int i = 0; i < 4; i++) t->sthr[k][i] = (unsigned)thr[2 * i] | ((unsigned)thr[2 * i + 1] << 16);
+        for (int i = 0; i < kSiThresholds / 2; i++)
+            t->ent[k].thr[i] = (unsigned)thr[2 * i] | ((unsigned)thr[2 * i + 1] << 16);
     }
     fc->use_thr = mono ? 1 : 0;
 }
