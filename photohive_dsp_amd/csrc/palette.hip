@@ -108,6 +108,15 @@ __device__ __forceinline__ unsigned short* img_chunks(const PaletteDev& o, long 
 
 typedef const __attribute__((address_space(1))) uint8_t gu8;
 
+// Byte b of pixel group st of w (registers; st is not a compile-time index).
+template <int kSteps>
+__device__ __forceinline__ int step_byte(const unsigned (&w)[kSteps][3], int st, int b) {
+    unsigned x = 0;
+#pragma unroll
+    for (int k = 0; k < kSteps; k++) x = k == st ? w[k][b >> 2] : x;
+    return (x >> (8 * (b & 3))) & 255;
+}
+
 // The 12 bytes of pixels p0..p0+3 of an image as three little-endian words.
 // Groups not wholly inside the image load from pixel 0 and are masked by the
 // caller (the `ok` bits); so every load is unconditional and stays in flight.
@@ -603,7 +612,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                 if (k == st) { cw[0] = w[k][0]; cw[1] = w[k][1]; cw[2] = w[k][2]; }
             // phases over the 4 pixels, so each step has 4 independent LDS reads
             // in flight: class entry -> group -> keep rule -> slot offset
-            int kr[4], kg[4], kb[4], sl[4];
+            int kr[4], kg[4], kb[4], sl[4], hN[4], hD[4];
             ClsEnt e[4];
             uint4 q[4];
             double o[4];
@@ -616,7 +625,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
             }
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int g = (ablate & 8) ? (kr[i] % tl) : classify_e<kThr>(kr[i], kg[i], kb[i], e[i], si8, gp, fc);
+                const int g = classify_e<kThr>(kr[i], kg[i], kb[i], e[i], si8, gp, fc, hN[i], hD[i]);
                 const int edge = g == -2;                    // exact group after the stream
                 emask |= (unsigned)(edge & (int)okg) << (4 * st + i);
                 q[i] = rec[edge ? tl : g];
@@ -630,11 +639,11 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
             }
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                // wrap(h + off) (calculate_avg_hsv, src/color_quantization.c:536-540): h from a
-                // reciprocal (within an ulp); the exact quotient decides the wrap whenever
-                // h + off is within 1e-9 of 0 or 360
+                // wrap(h + off) (calculate_avg_hsv, src/color_quantization.c:536-540): h = hN / hD
+                // through a reciprocal (within an ulp); the exact quotient decides the wrap
+                // whenever h + off is within 1e-9 of 0 or 360
                 const int kmx = max(kr[i], max(kg[i], kb[i])), kmn = min(kr[i], min(kg[i], kb[i]));
-                double tp = ((ablate & 32) ? 0.0 : hue_fast(kr[i], kg[i], kb[i])) + o[i];
+                double tp = ((ablate & 32) ? 0.0 : (double)hN[i] * inv_k(hD[i])) + o[i];
                 if (fabs(tp - 360.0) < 1e-9 || fabs(tp) < 1e-9) tp = hue_exact(kr[i], kg[i], kb[i], k255) + o[i];
                 tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
                 const int a = (sl[i] << cshift) | mycopy;
@@ -650,8 +659,9 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
         while (emask) {
             const int bt = __ffs(emask) - 1;
             emask &= emask - 1;
-            const long p = base + 4L * tid + 4L * kK1Threads * (bt >> 2) + (bt & 3);
-            const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
+            const int st = bt >> 2, i = bt & 3;
+            const long p = base + 4L * tid + 4L * kK1Threads * st + i;
+            const int kr = step_byte(w, st, 3 * i), kg = step_byte(w, st, 3 * i + 1), kb = step_byte(w, st, 3 * i + 2);
             const double hx = hue_exact(kr, kg, kb, k255);
             const int g = edge_group<kThr>(kr, kg, kb, hx, ent, si8, gp);
             const uint4 r = rec[g];

@@ -96,9 +96,12 @@ __device__ __forceinline__ int si_of(const ClsEnt& e, int kmx, int kd, const sig
 // classify() from the pixel's table entry (ent[max channel], read by the
 // caller so that several pixels' LDS reads are in flight together).
 // Branch-free: bitwise ands and selects only.
+// Also returns hN and hD: rgb2hsv's hue is hN / hD exactly (hD = max - min,
+// or hN = 0, hD = 1 for a gray pixel), so a caller that needs h for sums gets it
+// from one reciprocal.
 template <bool kThr>
 __device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& e, const signed char* si8g,
-                                          const GridParams& gp, const FastCls& F) {
+                                          const GridParams& gp, const FastCls& F, int& hN, int& hD) {
     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
     const int si = si_of<kThr>(e, kmx, kd, si8g);
     // hue bin
@@ -108,14 +111,26 @@ __device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& 
     const int base = isr ? (num < 0 ? 360 : 0) : (isg ? 120 : 240);
     const int kd1 = max(kd, 1);
     const int N = __mul24(base, kd1) + 60 * num, D = __mul24(F.lh, kd1);
+    hN = kd == 0 ? 0 : N;
+    hD = kd1;
     const int hi = (int)(((float)N + 0.5f) * __builtin_amdgcn_rcpf((float)D));
     const int special = (int)(num == 0) | (int)(num == kd) | (int)(num == -kd);
     const int edge = (special ^ 1) & (int)(__mul24(hi, D) == N);
     const int vi = (e.vpack << 16) >> 16, gray = e.vpack >> 16;
-    int g = __mul24(__mul24(hi, gp.sp) + si, gp.vp) + vi;
-    g = edge ? -2 : g;
-    g = si < 0 ? gray : g;
-    return vi < 0 ? gp.tl - 1 : g;
+    const int g = __mul24(__mul24(hi, gp.sp) + si, gp.vp) + vi;
+    // black (v < bt) > gray (s < gt) > edge > colour, as masks: a select chain
+    // here is turned into a branch around the whole hue arithmetic
+    const int mblack = -(int)(vi < 0);
+    const int mgray = -(int)(si < 0) & ~mblack;
+    const int medge = -edge & ~(mblack | mgray);
+    return (g & ~(mblack | mgray | medge)) | ((gp.tl - 1) & mblack) | (gray & mgray) | (-2 & medge);
+}
+
+template <bool kThr>
+__device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& e, const signed char* si8g,
+                                          const GridParams& gp, const FastCls& F) {
+    int hN, hD;
+    return classify_e<kThr>(kr, kg, kb, e, si8g, gp, F, hN, hD);
 }
 
 template <bool kThr>
