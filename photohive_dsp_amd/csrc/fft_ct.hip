@@ -8,23 +8,28 @@
 // unnormalised, e^{-i}), pgm_normalize_fft (:173-213) and the binning loop of
 // calculate_blur_profile (src/blur_profile.c:87-100).
 //
+// Intermediate layout (half spectrum after the row pass), tiled so that both
+// passes move whole 64-byte pieces: element (y, k) of row pair p = y/2 and
+// column pair kp = k/2 sits at ((p * KP + kp) * 2 + k%2) * 2 + y%2, with
+// KP = ceil((W/2+1) / 2).  A row pair's spectrum is one contiguous 64 KB run
+// (W = 4000); a column pair is 1500 pieces of 64 B (H = 3000).
+//
 // Row kernel (persistent, 2 blocks per CU).  Each step handles one pair of
 // image rows.  Both rows' RGB8 bytes were prefetched into registers (dwordx3 =
 // 4 pixels) during the previous step.  They become luma - avg and are packed
 // as one complex row (row y0 real, row y0+1 imaginary) in LDS.  The next pair's
 // loads are issued, then the FFT runs in LDS.  The two half spectra are
 // separated, A[k] = (Z[k] + conj Z[W-k]) / 2 and B[k] = (Z[k] - conj Z[W-k]) / 2i,
-// and stored column-major into inter[k][H].  The 4 pairs that share a 128-byte
-// line of every column run at the same time on one XCD, so the 32-byte pieces
-// merge in that XCD's L2.
+// and stored as the pair's contiguous tile row.
 //
-// Column kernel (persistent, 2 blocks per CU, a contiguous range of columns
-// per block).  The next column is prefetched into registers.  The last pass's
-// outputs never go back to LDS: the epilogue forms p = re^2 + im^2, keeps the
-// block's max and sums log(p) for p >= 1 into the element's polar bin.  Lanes
-// hold consecutive spectrum rows, so a wave covers few bins: one masked wave
-// sum and one LDS atomic per distinct bin.  The block adds its non-zero bins
-// to the image's bin sums at the end.
+// Column kernel (persistent, one block of 2 x T threads per CU, a contiguous
+// range of column pairs per block; each half of the block transforms one
+// column of the pair).  The next column pair is prefetched into registers.
+// The last pass's outputs never go back to LDS: the epilogue forms p = re^2 +
+// im^2, keeps the block's max and writes log(p) (p >= 1) per spectrum row to
+// LDS; each thread then sums a contiguous run of rows, one LDS atomic per
+// run of one polar bin.  The block adds its non-zero bins to the image's bin
+// sums at the end.
 //
 // log(p) for the bins: p = m * 2^e (frexp), log p = e ln2 + log(m) with log(m)
 // in fp32.  The absolute error is <= 2e-7 per element, against bin averages of
@@ -49,6 +54,8 @@ __device__ __forceinline__ double2 sel4(int e, double2 a, double2 b, double2 c, 
     return e == 0 ? a : (e == 1 ? b : (e == 2 ? c : d));
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // a native 128-bit register tuple
+
 constexpr double kWr = 0.299 / 255.0, kWg = 0.587 / 255.0, kWb = 0.114 / 255.0;
 
 __device__ __forceinline__ int byte_of(const unsigned (&w)[3], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255; }
@@ -64,7 +71,7 @@ struct RowK {
 };
 
 template <int W, int T, int... Rs>
-__global__ __launch_bounds__(T) void k_rows_ct(const uint8_t* __restrict__ img, int H,
+__global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* __restrict__ img, int H,
                                                const unsigned long long* __restrict__ sums,
                                                const double* __restrict__ k255g, const double2* __restrict__ twg,
                                                double2* __restrict__ inter, int ablate_arg) {
@@ -136,15 +143,18 @@ __global__ __launch_bounds__(T) void k_rows_ct(const uint8_t* __restrict__ img, 
         if (prn < P && !(ablate & 4)) fetch(prn);
         __syncthreads();
         if (!(ablate & 1)) fft_lds<W, T, 1, Rs...>(buf, tw, tid);
-        constexpr int WF = W / 2 + 1;
-        // lane pairs: lane 2j stores row y0's A[k], lane 2j+1 row y0+1's B[k] --
-        // one store instruction covers 32 columns x 32 contiguous bytes
-        for (int i = tid; i < 2 * WF && !(ablate & 2); i += T) {
-            const int k = i >> 1, second = i & 1;
-            const double2 zk = buf[k], zm = buf[k == 0 ? 0 : W - k];
-            const double2 o = second ? make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x))
-                                     : make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-            if (!second || two) inter[(size_t)k * H + y0 + second] = o;
+        constexpr int WF = W / 2 + 1, KP = (WF + 1) / 2;
+        // the pair's tile row, contiguous: thread i -> (column pair i/4, column
+        // k = 2(i/4) + (i/2)%2, row y0 + i%2); the phantom column WF (odd WF) is 0
+        double2* orow = inter + (size_t)pr * KP * 4;
+        for (int i = tid; i < 4 * KP && !(ablate & 2); i += T) {
+            const int k = 2 * (i >> 2) + ((i >> 1) & 1), second = i & 1;
+            const int kk = k < WF ? k : 0;
+            const double2 zk = buf[kk], zm = buf[kk == 0 ? 0 : W - kk];
+            double2 o = second ? make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x))
+                               : make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+            o = (k < WF && (two || !second)) ? o : make_double2(0.0, 0.0);
+            orow[i] = o;
         }
         __syncthreads();
         s++;
@@ -159,78 +169,123 @@ __device__ __forceinline__ double log_p(double p) {
     return (double)e * 0.69314718055994530942 + (double)__logf((float)m);
 }
 
-template <int H, int T, int... Rs>
+template <int H, int T, int CPB, int... Rs>
 struct ColK {
     using PL = Plan<H, T, 1, Rs...>;
     using L = typename PL::Last;
     static constexpr int R = Radices<Rs...>::count > 0 ? H / L::NB : 1;   // last radix
     static constexpr int NTW = tw_entries<1, Rs...>();
-    static constexpr int CR = (H + T - 1) / T;                            // prefetch rounds
+    static constexpr int P = (H + 1) / 2;                                 // row pairs
+    static constexpr int NT = CPB * T;                                    // block size
+    static constexpr int CR = (2 * CPB * P + NT - 1) / NT;                // prefetch rounds
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
-    static size_t lds(int nbins) { return sizeof(double2) * (H + NTW) + sizeof(double) * nbins; }
+    static size_t lds(int nbins) { return sizeof(double2) * (CPB * H + NTW) + sizeof(double) * nbins; }
     static_assert(Radices<Rs...>::product == H, "plan");
+    static_assert(CPB == 1 || CPB == 2, "columns per block");
+    static_assert(T % 2 == 0, "threads cover whole row pairs");
 };
 
-template <int H, int T, int... Rs>
-__global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter, int wf,
-                                               const uint16_t* __restrict__ binmap, int nbins,
-                                               double* __restrict__ bin_sums, double* __restrict__ fmax_part,
-                                               const double2* __restrict__ twg, double* __restrict__ dbg,
-                                               int ablate_arg) {
-    using K = ColK<H, T, Rs...>;
+// CPB == 2: one column pair per step; threads [0, T) take column 2kp, [T, 2T)
+// column 2kp+1.  CPB == 1: one column per block; blocks b and b ^ 8 (same XCD)
+// take the two columns of the same pairs, so each 64-byte tile is fetched once
+// into that XCD's L2 (the grid is a multiple of 16).
+// one-column blocks are sized for two resident blocks per CU
+template <int H, int T, int CPB, int... Rs>
+__global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) : 1) void k_cols_ct(const double2* __restrict__ inter, int wf,
+                                                     const uint16_t* __restrict__ binmap, int nbins,
+                                                     double* __restrict__ bin_sums, double* __restrict__ fmax_part,
+                                                     const double2* __restrict__ twg, double* __restrict__ dbg,
+                                                     int ablate_arg) {
+    using K = ColK<H, T, CPB, Rs...>;
     const int ablate = PHD_ABL(ablate_arg);
     using L = typename K::L;
-    constexpr int R = K::R;
+    constexpr int R = K::R, NT = K::NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double2* buf = reinterpret_cast<double2*>(smem);
-    double2* tw = buf + H;
+    double2* bufs = reinterpret_cast<double2*>(smem);         // [CPB][H]
+    double2* tw = bufs + CPB * H;
     double* lb = reinterpret_cast<double*>(tw + K::NTW);
     const int tid = threadIdx.x;
-    for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
-    for (int i = tid; i < nbins; i += T) lb[i] = 0.0;
-    const int c0 = (int)((long)blockIdx.x * wf / gridDim.x), c1 = (int)((long)(blockIdx.x + 1) * wf / gridDim.x);
-    double2 pf[K::CR];
-    auto fetch = [&](int col) {
-        const double2* src = inter + (size_t)col * H;
-#pragma unroll
-        for (int c = 0; c < K::CR; c++) {
-            const int i = tid + c * T;
-            if (H % T == 0 || i < H) pf[c] = src[i];
-        }
-    };
-    if (c0 < c1) fetch(c0);
+    const int half = CPB == 2 ? (tid >= T ? 1 : 0) : (int)((blockIdx.x >> 3) & 1);   // column of the pair
+    const int ht = CPB == 2 ? tid - half * T : tid;
+    double2* buf = bufs + (CPB == 2 ? half * H : 0);
+    for (int i = tid; i < K::NTW; i += NT) tw[i] = twg[i];
+    for (int i = tid; i < nbins; i += NT) lb[i] = 0.0;
+    const int kpn = (wf + 1) / 2;
+    const int nlog = CPB == 2 ? (int)gridDim.x : (int)gridDim.x / 2;
+    const int lblk = CPB == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
+    const int c0 = (int)((long)lblk * kpn / nlog), c1 = (int)((long)(lblk + 1) * kpn / nlog);
+    // the tiles: element 4p + 2c + r is (row 2p + r, column 2kp + c).  CPB == 2
+    // loads whole 64-B tiles (thread -> row pair tid/4, sub-element tid%4), CPB
+    // == 1 its column's 32-B half (row pair tid/2, row tid%2)
+    constexpr int PER = 2 * CPB;                               // elements of one row pair a block loads
+    // raw 16-byte words: the loads land in the registers the LDS stores read
+    // (no moves, so nothing waits for them before the next step)
+    u32x4 pf[K::CR];
+    const int prow0 = tid / PER, psub = CPB == 2 ? (tid & 3) : 2 * half + (tid & 1);
+#define PHD_COL_FETCH(kpv)                                                                  \
+    do {                                                                                    \
+        const u32x4* src_ = reinterpret_cast<const u32x4*>(inter) +                         \
+                            ((size_t)prow0 * kpn + (kpv)) * 4 + psub;                       \
+        _Pragma("unroll") for (int c = 0; c < K::CR; c++) {                                \
+            /* rows past the end re-read the last row pair (unused, no branch) */           \
+            const int pr_ = min(c * (NT / PER), K::P - 1 - prow0);                          \
+            pf[c] = src_[(size_t)pr_ * kpn * 4];                                            \
+        }                                                                                   \
+    } while (0)
+    if (c0 < c1) PHD_COL_FETCH(c0);
     double mx = 0.0;
     __syncthreads();
-    for (int col = c0; col < c1; col++) {
+    for (int kp = c0; kp < c1; kp++) {
+        {
+            u32x4* dst = reinterpret_cast<u32x4*>(bufs + (CPB == 2 ? ((psub >> 1) & 1) * H : 0) + 2 * prow0 +
+                                                  (psub & 1));
 #pragma unroll
-        for (int c = 0; c < K::CR; c++) {
-            const int i = tid + c * T;
-            if (H % T == 0 || i < H) buf[i] = pf[c];
+            for (int c = 0; c < K::CR; c++) {
+                const int y = 2 * (prow0 + c * (NT / PER)) + (psub & 1);
+                if (((PER * K::P) % NT == 0 || tid + c * NT < PER * K::P) && (H % 2 == 0 || y < H))
+                    dst[c * 2 * (NT / PER)] = pf[c];
+            }
         }
-        // bin ids of this thread's run of the column: u in [tid*E, tid*E + E)
-        uint16_t bm[K::E];
-        const uint16_t* bcol = binmap + (size_t)col * H + tid * K::E;
+        const int col = 2 * kp + half;
+        const bool live = col < wf;                       // the phantom column of an odd wf idles
+        // bin ids of this thread's run of its column: u in [ht*E, ht*E + E).  The
+        // table has 64 bytes of padding, so the last run may read past its end.
+        unsigned bmw[(K::E + 1) / 2];
+        {
+            const uint16_t* bcol = binmap + (size_t)(live ? col : 0) * H + ht * K::E;
+            if constexpr (K::E % 8 == 0 && (2 * H) % 16 == 0) {
 #pragma unroll
-        for (int j = 0; j < K::E; j++) bm[j] = (H % K::E == 0 && K::E * T == H) || tid * K::E + j < H ? bcol[j] : 0;
-        if (col + 1 < c1 && !(ablate & 4)) fetch(col + 1);
+                for (int j = 0; j < K::E / 8; j++) {
+                    const u32x4 t = reinterpret_cast<const u32x4*>(bcol)[j];
+                    bmw[4 * j] = t.x; bmw[4 * j + 1] = t.y; bmw[4 * j + 2] = t.z; bmw[4 * j + 3] = t.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < (K::E + 1) / 2; j++)
+                    bmw[j] = (unsigned)bcol[2 * j] | ((unsigned)bcol[2 * j + 1] << 16);
+            }
+        }
+        if (kp + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(kp + 1);
         __syncthreads();
-        if (!(ablate & 1)) K::PL::all_but_last(buf, tw, tid);
+        if (!(ablate & 1)) K::PL::all_but_last(buf, tw, ht);
         double2 v[L::ROUNDS][R];
-        L::load(buf, v, tid);
-        L::compute(v, tw + K::PL::last_tw_offset, tid);
+        if (!(ablate & 16)) {
+            L::load(buf, v, ht);
+            L::compute(v, tw + K::PL::last_tw_offset, ht);
+        }
         __syncthreads();                       // every thread has read its last-pass inputs
         double* lgb = reinterpret_cast<double*>(buf);   // log p per spectrum row, -1 for p < 1
 #pragma unroll
         for (int q = 0; q < L::ROUNDS; q++) {
-            const int b = tid + q * T;
-            if (L::active(b)) {
+            const int b = ht + q * T;
+            if (L::active(b) && !(ablate & 16)) {
 #pragma unroll
                 for (int k = 0; k < R; k++) {
                     const double2 X = v[q][k];
                     const double p = X.x * X.x + X.y * X.y;          // src/fft_processing.c:49
-                    mx = fmax(mx, p);
-                    if (dbg) dbg[(size_t)col * H + b + k * L::NB] = p;
-                    lgb[b + k * L::NB] = p >= 1 ? log_p(p) : -1.0;   // src/fft_processing.c:197-198
+                    if (live) mx = fmax(mx, p);
+                    if (dbg && live) dbg[(size_t)col * H + b + k * L::NB] = p;
+                    lgb[b + k * L::NB] = (live && p >= 1) ? log_p(p) : -1.0;   // src/fft_processing.c:197-198
                 }
             }
         }
@@ -242,11 +297,11 @@ __global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter
             double acc = 0.0;
 #pragma unroll
             for (int j = 0; j < K::E; j++) {
-                const int u = tid * K::E + j;
+                const int u = ht * K::E + j;
                 if ((H % K::E == 0 && K::E * T == H) || u < H) {
                     const double lg = lgb[u];
                     if (lg >= 0.0) {
-                        const int bin = bm[j];
+                        const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
                         if (bin != cur) {
                             if (cur >= 0) atomicAdd(&lb[cur], acc);
                             cur = bin;
@@ -260,17 +315,18 @@ __global__ __launch_bounds__(T) void k_cols_ct(const double2* __restrict__ inter
         }
         __syncthreads();
     }
+#undef PHD_COL_FETCH
     // block max -> one partial per block; non-zero bins -> the image's sums
     mx = wave_max(mx);
-    double* red = reinterpret_cast<double*>(buf);
+    double* red = reinterpret_cast<double*>(bufs);
     if (lane_id() == 0) red[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
         double m = 0.0;
-        for (int w = 0; w < T / 64; w++) m = fmax(m, red[w]);
+        for (int w = 0; w < (NT + 63) / 64; w++) m = fmax(m, red[w]);
         fmax_part[blockIdx.x] = m;
     }
-    for (int i = tid; i < nbins; i += T) {
+    for (int i = tid; i < nbins && !(ablate & 8); i += NT) {
         const double t = lb[i];
         if (t != 0.0) atomicAdd(&bin_sums[i], t);
     }
@@ -304,17 +360,21 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
     return hipGetLastError();
 }
 
-template <int H, int T, int... Rs>
+template <int H, int T, int CPB, int... Rs>
 int cols_grid(int wf, int nbins) {
-    const int g = resident_grid(k_cols_ct<H, T, Rs...>, T, ColK<H, T, Rs...>::lds(nbins));
-    return wf < g ? wf : g;
+    int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, CPB * T, ColK<H, T, CPB, Rs...>::lds(nbins));
+    const int kpn = (wf + 1) / 2;
+    if (CPB == 2) return kpn < g ? kpn : g;
+    g = g / 16 * 16;                                        // XCD partner blocks b, b ^ 8
+    return g < 16 ? 16 : g;
 }
 
-template <int H, int T, int... Rs>
+template <int H, int T, int CPB, int... Rs>
 hipError_t cols_ct(const double2* inter, int wf, const uint16_t* binmap, int nbins, double* bin_sums,
                    double* fmax_part, const double2* tw, double* dbg, hipStream_t st) {
-    const size_t lds = ColK<H, T, Rs...>::lds(nbins);
-    hipLaunchKernelGGL((k_cols_ct<H, T, Rs...>), dim3(cols_grid<H, T, Rs...>(wf, nbins)), dim3(T), lds, st, inter,
+    const size_t lds = ColK<H, T, CPB, Rs...>::lds(nbins);
+    hipLaunchKernelGGL((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3(CPB * T), lds,
+                       st, inter,
                        wf, binmap, nbins, bin_sums, fmax_part, tw, dbg, g_ablate);
     return hipGetLastError();
 }
@@ -352,11 +412,14 @@ bool ct_rows_plan(int w, std::vector<int>* radices) {
     return false;
 }
 
+template <int CPB, int... Rs>
+std::vector<int> col_radices() { return std::vector<int>{Rs...}; }
+
 bool ct_cols_plan(int h, std::vector<int>* radices) {
     const int n_ = h;
 #define PHD_X(N, V, T, ...)                                          \
     if (n_ == N && V == v_) {                                        \
-        if (radices) *radices = std::vector<int>{__VA_ARGS__};       \
+        if (radices) *radices = col_radices<__VA_ARGS__>();          \
         return true;                                                 \
     }
     PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);

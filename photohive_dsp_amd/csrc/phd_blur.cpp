@@ -94,7 +94,9 @@ bool build_blur_table(int height, int width, int nr, int na, BlurTable* t) {
     t->counts.assign((size_t)na * nr, 0);
     for (unsigned i = 0; i < nth; i++)
         for (size_t b = 0; b < t->counts.size(); b++) t->counts[b] += part[i][b];
-    if (hipMalloc(&t->d_map, map.size() * sizeof(uint16_t)) != hipSuccess) {
+    // + 64 bytes: the FFT column kernel loads each thread's run of bin ids with
+    // 16-byte loads that may read past the last column's end
+    if (hipMalloc(&t->d_map, map.size() * sizeof(uint16_t) + 64) != hipSuccess) {
         set_error("hipMalloc of the blur bin table failed");
         return false;
     }

@@ -141,18 +141,18 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 // The first radix is odd (LDS bank-conflict-free first pass, fft_engine.h).
 // Rows need length % 4 == 0.
 #define PHD_CT_ROWS(X)              \
-    X(4000, 0, 256, 25, 16, 10)     \
-    X(4000, 1, 256, 25, 20, 8)      \
+    X(4000, 0, 512, 5, 8, 10, 10)   \
+    X(4000, 1, 256, 25, 16, 10)     \
     X(4000, 2, 512, 25, 16, 10)     \
-    X(4000, 3, 400, 25, 16, 10)     \
-    X(4000, 4, 320, 25, 16, 10)
-#define PHD_CT_COLS(X)              \
-    X(3000, 0, 256, 15, 20, 10)     \
-    X(3000, 1, 256, 25, 12, 10)     \
-    X(3000, 2, 320, 15, 20, 10)     \
-    X(3000, 3, 512, 15, 20, 10)     \
-    X(3000, 4, 192, 25, 12, 10)     \
-    X(3000, 5, 300, 25, 12, 10)
+    X(4000, 3, 512, 5, 10, 8, 10)
+// columns: X(length, variant, threads per column, columns per block, radices...)
+#define PHD_CT_COLS(X)                 \
+    X(3000, 0, 384, 2, 5, 6, 10, 10)   \
+    X(3000, 1, 256, 1, 15, 20, 10)     \
+    X(3000, 2, 384, 1, 5, 6, 10, 10)   \
+    X(3000, 3, 512, 1, 5, 6, 10, 10)   \
+    X(3000, 4, 256, 2, 15, 20, 10)     \
+    X(3000, 5, 512, 2, 5, 6, 10, 10)
 int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);

@@ -298,7 +298,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const int ncolblocks = fs.col_blocks;
     const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
-        !ensure_device((void**)&c->d_inter, &c->inter_bytes, sizeof(double2) * (size_t)height * wf))
+        !ensure_device((void**)&c->d_inter, &c->inter_bytes, sizeof(double2) * (size_t)(height + 1) * (wf + 1)))
         return false;
     uint8_t* dw = (uint8_t*)c->d_ws;
     uint8_t* hp = (uint8_t*)c->h_pin;
