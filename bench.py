@@ -26,7 +26,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -40,7 +40,7 @@ def parse():
                    help="do not bracket kernels with HIP events (roofline then null)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                    help="per-kernel PMC traffic summary written by tools/pmc_collect.py")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def cpu_baseline(h, w, n_images):
@@ -172,19 +172,22 @@ def main():
     }
     line["roofline"] = None
     if dom in kern:
-        ab = algorithmic_bytes(dom, H, W)
+        # the palette passes take the whole batch in one launch, the FFT passes one image
+        per_launch = B * args.steps / kern[dom]["launches"]
+        ab = algorithmic_bytes(dom, H, W) * per_launch
         achieved = ab / (kern[dom]["avg_us"] * 1e-6) / 1e9
         traffic = None
         try:
             with open(args.pmc) as f:
                 pm = json.load(f)
             if pm.get("image") == f"{H}x{W}" and dom in pm.get("kernels", {}):
-                traffic = pm["kernels"][dom]["hbm_bytes_per_launch"]
-        except (OSError, ValueError):
+                traffic = pm["kernels"][dom]["hbm_bytes_per_image"] * per_launch
+        except (OSError, ValueError, KeyError):
             pass
         line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                             "traffic": traffic, "algorithmic_bytes_per_launch": ab,
+                            "images_per_launch": per_launch,
                             "avg_launch_us": round(kern[dom]["avg_us"], 2)}
         line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
     if not args.no_cpu_baseline:

@@ -20,7 +20,9 @@ namespace phd {
 namespace {
 
 // LDS carve of K1 (one dynamic array, 16-B aligned base: no static __shared__).
-constexpr int kK1Threads = 1024;             // K1 block: 16 waves over one kChunk
+constexpr int kK1Threads = 1024;             // Kcut block: 16 waves over one kChunk
+constexpr int kPalThreads = 512;             // K1 block: 8 waves, two resident per CU
+constexpr int kK3Threads = 1024;             // K3 block: one per CU (its LDS sums want the room)
 struct K1Lds {
     static constexpr int k255 = 0;           // 256 doubles
     static constexpr int ent = 2048;         // 256 ClsEnt (16 B)
@@ -106,6 +108,18 @@ __device__ __forceinline__ unsigned short* img_chunks(const PaletteDev& o, long 
     return reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(o.chunk_hist) + i * h_stride);
 }
 
+__device__ __forceinline__ double* img_gsum(const PaletteDev& o, long a_stride, int i) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(o.gsum) + i * a_stride);
+}
+__device__ __forceinline__ unsigned* img_gcell(const PaletteDev& o, long a_stride, int i) {
+    return reinterpret_cast<unsigned*>(reinterpret_cast<char*>(o.gcell) + i * a_stride);
+}
+
+// Bytes of K1's chunk-count copies and run counts (the fused sums follow, 8-B aligned).
+__host__ __device__ __forceinline__ int k1_count_bytes(int tl, int cshift) {
+    return (4 * (2 * (tl + 1) * (1 << cshift) + tl) + 15) & ~15;
+}
+
 typedef const __attribute__((address_space(1))) uint8_t gu8;
 
 // Byte b of pixel group st of w (registers; st is not a compile-time index).
@@ -160,8 +174,13 @@ __device__ __forceinline__ void load_group(const uint8_t* ip, long p0, bool ok, 
 // image end are masked to (0, 0, 0) pixels, which add nothing to the moments
 // or sum(s) and are taken back out of the histogram; the < 4 pixels of a
 // partial final group are done by one thread of the last chunk.
-template <bool kHist, bool kAligned, bool kThr>
-__global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_MINWAVES) void k_hsv_stats(
+//
+// kSums (the fused palette pass, needs kHist): per group, also sum(h), sum(s),
+// sum(v) and the counts per hue cell (HueCells), so calculate_avg_hsv's slot
+// sums of every group kept whole follow on the host without a second pass.
+// They have the same C lane-private copies and are flushed with the run.
+template <bool kHist, bool kSums, bool kAligned, bool kThr>
+__global__ __launch_bounds__(kPalThreads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_MINWAVES) void k_hsv_stats(
         const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
         const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, PaletteDev out, long a_stride,
         long h_stride, int cshift, int ablate_arg) {
@@ -176,17 +195,24 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
     const int C = 1 << cshift, cm = C - 1;
     unsigned* lh = reinterpret_cast<unsigned*>(smem + K1Lds::area);   // [2][tl1][C] chunk counts
     unsigned* seg = lh + 2 * tl1 * C;                                  // [tl] counts of the run
+    const int ncell = HueCells::count(gp);
+    double* acc = reinterpret_cast<double*>(smem + K1Lds::area + k1_count_bytes(tl, cshift));  // [3][tl1][C]
+    unsigned* cel = reinterpret_cast<unsigned*>(acc + 3 * tl1 * C);   // [ncell + 1][C]
     const int tid = threadIdx.x;
     const int mycopy = tid & cm;
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
     stage_tables(smem, k255g, tabs);
     if (kHist) {
-        for (int i = tid; i < 2 * tl1 * C + tl; i += kK1Threads) lh[i] = 0;
+        for (int i = tid; i < 2 * tl1 * C + tl; i += kPalThreads) lh[i] = 0;
+    }
+    if (kSums) {
+        for (int i = tid; i < 3 * tl1 * C; i += kPalThreads) acc[i] = 0.0;
+        for (int i = tid; i < (ncell + 1) * C; i += kPalThreads) cel[i] = 0;
     }
     __syncthreads();
 
-    constexpr int kSteps = kChunk / (4 * kK1Threads);
+    constexpr int kSteps = kChunk / (4 * kPalThreads);
     static_assert(kSteps >= 2 && kSteps <= 8, "K1 step count");
     const long full_end = npix & ~3L;                       // groups wholly inside the image
     unsigned w[kSteps][3];
@@ -195,7 +221,7 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
         okb = 0;
 #pragma unroll
         for (int st = 0; st < kSteps; st++) {
-            const long p0 = (long)c * kChunk + 4L * tid + 4L * kK1Threads * st;
+            const long p0 = (long)c * kChunk + 4L * tid + 4L * kPalThreads * st;
             const bool ok = p0 < full_end;
             okb |= (unsigned)ok << st;
             load_group<kAligned>(ip, p0, ok, w[st]);
@@ -236,8 +262,21 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int kmx = max(kr[i], max(kg[i], kb[i])), kmn = min(kr[i], min(kg[i], kb[i]));
-                if (!(ablate & 32)) ssum += sat_of(kmx, kmn);
-                if (kHist) {
+                const double sv = sat_of(kmx, kmn);
+                if (!(ablate & 32)) ssum += sv;
+                if (kSums) {
+                    int hN, hD, cell;
+                    const int g = classify_f<kThr>(kr[i], kg[i], kb[i], e[i], si8, gp, fc, hN, hD, cell);
+                    // a non-special hue on a half-bin boundary (g == -2): after the stream
+                    const int edge = g == -2;
+                    emask |= (unsigned)edge << (4 * st + i);
+                    const int a = ((edge ? tl : g) << cshift) | mycopy;
+                    atomicAdd(&ch[a], 1u);
+                    atomicAdd(&acc[a], (double)hN * inv_k(hD));
+                    atomicAdd(&acc[tl1 * C + a], sv);
+                    atomicAdd(&acc[2 * tl1 * C + a], v_fast(kmx));
+                    atomicAdd(&cel[(cell << cshift) | mycopy], 1u);
+                } else if (kHist) {
                     const int g = (ablate & 8) ? (kr[i] % tl) : classify_e<kThr>(kr[i], kg[i], kb[i], e[i], si8, gp, fc);
                     // a hue exactly on a bin edge (g == -2): counted after the stream
                     const int edge = g == -2;
@@ -264,7 +303,20 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
                 sr += kr; sg += kg; sb += kb;
                 qr += kr * kr; qg += kg * kg; qb += kb * kb;
                 double sv;
-                if (kHist) {
+                if (kSums) {
+                    const int kmx = max(kr, max(kg, kb));
+                    sv = sat_of(kmx, min(kr, min(kg, kb)));
+                    int hN, hD, cell;
+                    double h;
+                    int g = classify_f<kThr>(kr, kg, kb, ent[kmx], si8, gp, fc, hN, hD, cell);
+                    if (g == -2) g = fused_exact(kr, kg, kb, k255, gp, fc.lh, h, cell);
+                    else h = (double)hN * inv_k(hD);
+                    atomicAdd(&ch[g << cshift], 1u);
+                    atomicAdd(&acc[g << cshift], h);
+                    atomicAdd(&acc[(tl1 * C) + (g << cshift)], sv);
+                    atomicAdd(&acc[(2 * tl1 * C) + (g << cshift)], v_fast(kmx));
+                    atomicAdd(&cel[cell << cshift], 1u);
+                } else if (kHist) {
                     int g = classify<kThr>(kr, kg, kb, ent, si8, gp, fc, sv);
                     if (g == -2) g = exact_group(kr, kg, kb, k255, gp);
                     atomicAdd(&ch[g << cshift], 1u);
@@ -278,9 +330,23 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
         while (kHist && emask) {
             const int bt = __ffs(emask) - 1;
             emask &= emask - 1;
-            const long p = base + 4L * tid + 4L * kK1Threads * (bt >> 2) + (bt & 3);
-            const int g = exact_group(ip[3 * p], ip[3 * p + 1], ip[3 * p + 2], k255, gp);
-            atomicAdd(&ch[(g << cshift) | mycopy], 1u);
+            const long p = base + 4L * tid + 4L * kPalThreads * (bt >> 2) + (bt & 3);
+            const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
+            if (kSums) {
+                double h;
+                int cell;
+                const int g = fused_exact(kr, kg, kb, k255, gp, fc.lh, h, cell);
+                const int kmx = max(kr, max(kg, kb));
+                const int a = (g << cshift) | mycopy;
+                atomicAdd(&ch[a], 1u);
+                atomicAdd(&acc[a], h);
+                atomicAdd(&acc[tl1 * C + a], sat_of(kmx, min(kr, min(kg, kb))));
+                atomicAdd(&acc[2 * tl1 * C + a], v_fast(kmx));
+                atomicAdd(&cel[(cell << cshift) | mycopy], 1u);
+            } else {
+                const int g = exact_group(kr, kg, kb, k255, gp);
+                atomicAdd(&ch[(g << cshift) | mycopy], 1u);
+            }
         }
         // next work item: prefetch its pixels now
         const int cimg = img, cc = c;
@@ -299,12 +365,17 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
             if (pad > 0 && tid == 0) {
                 double sv;
                 atomicSub(&ch[classify<kThr>(0, 0, 0, ent, si8, gp, fc, sv) << cshift], (unsigned)pad);
+                if (kSums) {
+                    int hN, hD, cell;
+                    (void)classify_f<kThr>(0, 0, 0, ent[0], si8, gp, fc, hN, hD, cell);
+                    atomicSub(&cel[cell << cshift], (unsigned)pad);
+                }
             }
             __syncthreads();
             // fold the C copies of each group (C consecutive lanes) with shuffles
             unsigned short* chunk_out = img_chunks(out, h_stride, cimg) + (long)cc * tl;
             const int ncopy = (ablate & 64) ? 0 : tl << cshift;
-            for (int i0 = tid; i0 < ((ncopy + kK1Threads - 1) & ~(kK1Threads - 1)); i0 += kK1Threads) {
+            for (int i0 = tid; i0 < ((ncopy + kPalThreads - 1) & ~(kPalThreads - 1)); i0 += kPalThreads) {
                 unsigned n = 0;
                 if (i0 < ncopy) {
                     n = ch[i0];
@@ -336,19 +407,49 @@ __global__ __launch_bounds__(kK1Threads, kHist ? PHD_K1_MINWAVES_HIST : PHD_K1_M
             __syncthreads();
             if (tid < 6) {
                 unsigned long long t = 0;
-                for (int q = 0; q < kK1Threads / 64; q++) t += red[q * 8 + tid];
+                for (int q = 0; q < kPalThreads / 64; q++) t += red[q * 8 + tid];
                 if (!(ablate & 128)) atomicAdd(&img_sums(out, a_stride, cimg)[tid], t);
             } else if (tid == 6) {
                 double t = 0.0;
-                for (int q = 0; q < kK1Threads / 64; q++) t += reinterpret_cast<double*>(red)[q * 8 + 6];
+                for (int q = 0; q < kPalThreads / 64; q++) t += reinterpret_cast<double*>(red)[q * 8 + 6];
                 img_spart(out, a_stride, cimg)[seg_c0] = t;   // one slot per run (host sums them)
             }
             if (kHist) {
                 unsigned* hist = img_hist(out, a_stride, cimg);
-                for (int i = tid; i < tl; i += kK1Threads) {
+                for (int i = tid; i < tl; i += kPalThreads) {
                     const unsigned n = seg[i];
                     if (n && !(ablate & 128)) atomicAdd(&hist[i], n);
                     seg[i] = 0;
+                }
+            }
+            if (kSums) {
+                // fold the C copies (consecutive lanes) of the sums and cell counts;
+                // the deferred-pixel dummies (group tl, cell ncell) are just zeroed
+                double* gsum = img_gsum(out, a_stride, cimg);
+                unsigned* gcell = img_gcell(out, a_stride, cimg);
+                const int nacc = 3 * tl1 * C;
+                for (int i0 = tid; i0 < ((nacc + kPalThreads - 1) & ~(kPalThreads - 1)); i0 += kPalThreads) {
+                    double a = 0.0;
+                    if (i0 < nacc) {
+                        a = acc[i0];
+                        acc[i0] = 0.0;
+                    }
+                    for (int o = 1; o < C; o <<= 1) a += __shfl_xor(a, o, 64);
+                    if (i0 < nacc && (i0 & cm) == 0) {
+                        const int f = i0 / (tl1 * C), g = (i0 - f * tl1 * C) >> cshift;
+                        if (g < tl && a != 0.0) atomicAdd(&gsum[f * tl + g], a);
+                    }
+                }
+                const int ncel = (ncell + 1) * C;
+                for (int i0 = tid; i0 < ((ncel + kPalThreads - 1) & ~(kPalThreads - 1)); i0 += kPalThreads) {
+                    unsigned n = 0;
+                    if (i0 < ncel) {
+                        n = cel[i0];
+                        cel[i0] = 0;
+                    }
+                    for (int o = 1; o < C; o <<= 1) n += __shfl_xor(n, o, 64);
+                    const int q = i0 >> cshift;
+                    if (i0 < ncel && (i0 & cm) == 0 && q < ncell && n) atomicAdd(&gcell[q], n);
                 }
             }
             sr = sg = sb = qr = qg = qb = 0;
@@ -535,7 +636,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
 // distinct banks), whatever the image.  Per image, the copies are folded and
 // go to HBM with one atomic per slot and field.
 template <bool kAligned, bool kThr>
-__global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
+__global__ __launch_bounds__(kK3Threads, 4) void k_palette_sums_b(
         const uint8_t* const* __restrict__ imgs, long npix, int nchunks, long nitems, GridParams gp, FastCls fc,
         const ClassTables* __restrict__ tabs, const double* __restrict__ k255g,
         const GroupRule* __restrict__ rules0, const double* __restrict__ off0, long b_stride,
@@ -560,7 +661,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
     stage_tables(smem, k255g, tabs);
-    for (int i = tid; i < ms * C; i += kK1Threads) {
+    for (int i = tid; i < ms * C; i += kK3Threads) {
         acc[i] = acc[ms * C + i] = acc[2 * ms * C + i] = 0.0;
         cnt[i] = 0;
     }
@@ -569,7 +670,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
         off[max_slots] = 0.0;
     }
 
-    constexpr int kSteps = kChunk / (4 * kK1Threads);
+    constexpr int kSteps = kChunk / (4 * kK3Threads);
     const long full_end = npix & ~3L;
     int img = (int)(it0 / nchunks), c = (int)(it0 - (long)img * nchunks);
     int cur = -1, ns = 0;
@@ -579,7 +680,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                     reinterpret_cast<const GroupRule*>(reinterpret_cast<const char*>(rules0) + img * b_stride);
             const double* offi = reinterpret_cast<const double*>(reinterpret_cast<const char*>(off0) + img * b_stride);
             ns = nslots_img[img];
-            for (int i = tid; i < tl; i += kK1Threads) {
+            for (int i = tid; i < tl; i += kK3Threads) {
                 const GroupRule r = rules[i];
                 uint4 q;
                 q.x = (unsigned)r.slot;
@@ -588,8 +689,8 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
                 q.w = 0;
                 rec[i] = q;
             }
-            for (int i = tid; i < ns; i += kK1Threads) off[i] = offi[i];
-            for (int i = ns + tid; i < max_slots; i += kK1Threads) off[i] = 0.0;
+            for (int i = tid; i < ns; i += kK3Threads) off[i] = offi[i];
+            for (int i = ns + tid; i < max_slots; i += kK3Threads) off[i] = 0.0;
             cur = img;
             __syncthreads();
         }
@@ -598,13 +699,13 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
         unsigned w[kSteps][3];
 #pragma unroll
         for (int st = 0; st < kSteps; st++) {
-            const long p0 = base + 4L * tid + 4L * kK1Threads * st;
+            const long p0 = base + 4L * tid + 4L * kK3Threads * st;
             load_group<kAligned>(ip, p0, p0 < full_end, w[st]);
         }
         unsigned emask = 0;                                  // this thread's edge pixels (bit 4*st + i)
 #pragma unroll 1
         for (int st = 0; st < kSteps; st++) {
-            const long p0 = base + 4L * tid + 4L * kK1Threads * st;
+            const long p0 = base + 4L * tid + 4L * kK3Threads * st;
             const bool okg = p0 < full_end;
             unsigned cw[3];
 #pragma unroll
@@ -660,7 +761,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
             const int bt = __ffs(emask) - 1;
             emask &= emask - 1;
             const int st = bt >> 2, i = bt & 3;
-            const long p = base + 4L * tid + 4L * kK1Threads * st + i;
+            const long p = base + 4L * tid + 4L * kK3Threads * st + i;
             const int kr = step_byte(w, st, 3 * i), kg = step_byte(w, st, 3 * i + 1), kb = step_byte(w, st, 3 * i + 2);
             const double hx = hue_exact(kr, kg, kb, k255);
             const int g = edge_group<kThr>(kr, kg, kb, hx, ent, si8, gp);
@@ -712,7 +813,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
             // consecutive lanes and fold with shuffles
             const int ncopy = ns << cshift;
             const int total = 4 * ncopy;
-            for (int i0 = tid; i0 < ((total + kK1Threads - 1) & ~(kK1Threads - 1)); i0 += kK1Threads) {
+            for (int i0 = tid; i0 < ((total + kK3Threads - 1) & ~(kK3Threads - 1)); i0 += kK3Threads) {
                 const int f = i0 / max(ncopy, 1), j = i0 - f * ncopy;
                 double a = 0.0;
                 if (i0 < total) {
@@ -730,6 +831,94 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_palette_sums_b(
             }
             __syncthreads();
         }
+    }
+}
+
+// Partial-group sums of the fused palette (downsample_rate == 1): the groups a
+// tie sent to a parent's tail node keep only their first `keep` pixels in
+// raster order plus, maybe, their last one (group_irregular_pixels,
+// src/color_quantization.c:435-447; the cutoff and last index come from Kcut).
+// Blocks (entry, split) walk the 4096-pixel units before the cutoff whose chunk
+// holds pixels of the group (K1's chunk counts), split-strided, and add calculate_avg_hsv's
+// terms of the kept pixels (:536-550: wrap(h + off), s, v, count) in
+// registers; one atomic per field and block.  Typical partial groups keep a
+// few hundred pixels of their first chunks.
+constexpr int kPartThreads = 256;
+template <bool kAligned, bool kThr>
+__global__ __launch_bounds__(kPartThreads) void k_partial_sums_b(
+        const uint8_t* const* __restrict__ imgs, long npix, GridParams gp, FastCls fc,
+        const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, const int2* __restrict__ entries,
+        const unsigned short* __restrict__ chunk_hist0, long h_stride, const GroupRule* __restrict__ rules0,
+        const double* __restrict__ off0, long b_stride, double* out0, long c_stride) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
+    const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
+    double* red = reinterpret_cast<double*>(smem + K1Lds::red);       // [4 waves][4]
+    const signed char* si8 = tabs->si8;
+    const int tid = threadIdx.x;
+    stage_tables(smem, k255g, tabs);
+    __syncthreads();
+    const int img = entries[blockIdx.x].x, g = entries[blockIdx.x].y;
+    const uint8_t* ip = imgs[img];
+    const GroupRule r = reinterpret_cast<const GroupRule*>(reinterpret_cast<const char*>(rules0) + img * b_stride)[g];
+    const double off = reinterpret_cast<const double*>(reinterpret_cast<const char*>(off0) + img * b_stride)[r.slot];
+    const unsigned short* chunk_hist =
+            reinterpret_cast<const unsigned short*>(reinterpret_cast<const char*>(chunk_hist0) + img * h_stride);
+    const int tl = gp.tl;
+    const unsigned cut = (r.partial && r.keep > 0) ? r.cutoff : 0u;
+    const long full_end = npix & ~3L;
+    double th = 0.0, ts = 0.0, tv = 0.0, tn = 0.0;
+    auto add = [&](int kr, int kg, int kb) {
+        double sv;
+        if (exact_group_t<kThr>(kr, kg, kb, ent, si8, k255, gp, fc, sv) != g) return;
+        double tp = hue_exact(kr, kg, kb, k255) + off;
+        tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+        th += tp;
+        ts += sv;
+        tv += v_of(max(kr, max(kg, kb)), k255);
+        tn += 1.0;
+    };
+    // units of kPartUnit pixels (4 groups of 4 per thread, loads issued together)
+    constexpr int kUnit = 16 * kPartThreads;
+    static_assert(kChunk % kUnit == 0, "units tile a chunk");
+    const long umax = cut > 0 ? (long)(cut - 1) / kUnit : -1;
+    for (long u = blockIdx.y; u <= umax; u += gridDim.y) {
+        if (chunk_hist[(u * kUnit / kChunk) * tl + g] == 0) continue;   // block-uniform
+        const long end = std::min<long>((u + 1) * kUnit, (long)cut);
+        unsigned w[4][3];
+        bool okg[4];
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            const long p0 = u * kUnit + 4L * tid + 4L * kPartThreads * st;
+            okg[st] = p0 + 3 < full_end;
+            load_group<kAligned>(ip, p0, okg[st], w[st]);
+        }
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            const long p0 = u * kUnit + 4L * tid + 4L * kPartThreads * st;
+            if (p0 >= end) continue;
+            if (okg[st]) {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (p0 + i < end) add(px_byte(w[st], 3 * i), px_byte(w[st], 3 * i + 1), px_byte(w[st], 3 * i + 2));
+            } else {
+                for (long p = p0; p < p0 + 4 && p < end && p < npix; p++) add(ip[3 * p], ip[3 * p + 1], ip[3 * p + 2]);
+            }
+        }
+    }
+    if (blockIdx.y == 0 && tid == 0 && r.partial && r.dangle && r.last != 0xFFFFFFFFu && r.last >= cut) {
+        const long p = r.last;                               // the dangling node's pixel
+        add(ip[3 * p], ip[3 * p + 1], ip[3 * p + 2]);
+    }
+    const double v4[4] = {wave_sum(th), wave_sum(ts), wave_sum(tv), wave_sum(tn)};
+    if (lane_id() == 0)
+        for (int f = 0; f < 4; f++) red[(tid >> 6) * 4 + f] = v4[f];
+    __syncthreads();
+    if (tid < 4) {
+        double a = 0.0;
+        for (int q = 0; q < kPartThreads / 64; q++) a += red[q * 4 + tid];
+        double* out = reinterpret_cast<double*>(reinterpret_cast<char*>(out0) + img * c_stride);
+        if (a != 0.0) atomicAdd(&out[4 * r.slot + tid], a);
     }
 }
 
@@ -1063,45 +1252,61 @@ int k3_cshift(int max_slots) {
     return c;
 }
 
-size_t hsv_stats_lds(const GridParams& gp, bool hist) {
-    return hist ? K1Lds::area + sizeof(unsigned) * (2 * ((size_t)gp.tl + 1) * (1u << k1_cshift(gp.tl)) + gp.tl)
-                : (size_t)K1Lds::red + 1024;
+// LDS of K1: tables, chunk-count copies, run counts and (fused) the sums and
+// cell-count copies.
+size_t k1_lds_bytes(const GridParams& gp, int cshift, bool sums) {
+    const size_t C = (size_t)1 << cshift;
+    return (size_t)K1Lds::area + k1_count_bytes(gp.tl, cshift) +
+           (sums ? 8 * 3 * ((size_t)gp.tl + 1) * C + 4 * ((size_t)HueCells::count(gp) + 1) * C : 0);
+}
+
+// Fused K1's copies: the most (<= 16) with two blocks per CU, else one copy in
+// one block per CU, else -1 (the palette takes the two-pass path).
+int k1_fused_cshift(const GridParams& gp) {
+    for (int c = 4; c >= 0; c--)
+        if (k1_lds_bytes(gp, c, true) <= 78 * 1024) return c;
+    return k1_lds_bytes(gp, 0, true) <= 150 * 1024 ? 0 : -1;
+}
+
+bool fused_palette_ok(const GridParams& gp) { return k1_fused_cshift(gp) >= 0; }
+
+size_t hsv_stats_lds(const GridParams& gp, bool hist, bool sums) {
+    if (sums) return k1_lds_bytes(gp, k1_fused_cshift(gp), true);
+    return hist ? k1_lds_bytes(gp, k1_cshift(gp.tl), false) : (size_t)K1Lds::red + 1024;
 }
 
 hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width,
                                   const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
                                   const PaletteDev& out0, long a_stride, long h_stride, int nchunks,
-                                  const double* k255, bool hist, bool aligned, hipStream_t st) {
+                                  const double* k255, bool hist, bool sums, bool aligned, hipStream_t st) {
     const long npix = (long)height * width;
     const long nitems = (long)n * nchunks;
-    const size_t lds = hsv_stats_lds(gp, hist);
-    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
+    if (sums && (!hist || !fused_palette_ok(gp))) return hipErrorInvalidValue;
+    const size_t lds = hsv_stats_lds(gp, hist, sums);
+    const int cshift = sums ? k1_fused_cshift(gp) : k1_cshift(gp.tl);
+    const void* kfn = nullptr;
+#define PHD_K1_FN(H, S, A, T) (const void*)k_hsv_stats<H, S, A, T>
+    if (sums)
+        kfn = fc.use_thr ? (aligned ? PHD_K1_FN(true, true, true, true) : PHD_K1_FN(true, true, false, true))
+                         : (aligned ? PHD_K1_FN(true, true, true, false) : PHD_K1_FN(true, true, false, false));
+    else if (hist)
+        kfn = fc.use_thr ? (aligned ? PHD_K1_FN(true, false, true, true) : PHD_K1_FN(true, false, false, true))
+                         : (aligned ? PHD_K1_FN(true, false, true, false) : PHD_K1_FN(true, false, false, false));
+    else
+        kfn = aligned ? PHD_K1_FN(false, false, true, true) : PHD_K1_FN(false, false, false, true);
+#undef PHD_K1_FN
+    // persistent blocks: as many as are resident at once
+    (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kPalThreads, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
-#define PHD_K1_LAUNCH(H, A, T)                                                                                   \
-    do {                                                                                                      \
-        static bool attr = false;                                                                             \
-        if (!attr) {                                                                                          \
-            (void)hipFuncSetAttribute((const void*)k_hsv_stats<H, A, T>,                                      \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                \
-            attr = true;                                                                                      \
-        }                                                                                                     \
-        hipLaunchKernelGGL((k_hsv_stats<H, A, T>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix, nchunks, \
-                           nitems, gp, fc, tabs, k255, out0, a_stride, h_stride, k1_cshift(gp.tl), env_ablate()); \
-    } while (0)
-    if (hist) {
-        if (fc.use_thr) {
-            if (aligned) PHD_K1_LAUNCH(true, true, true);
-            else PHD_K1_LAUNCH(true, false, true);
-        } else {
-            if (aligned) PHD_K1_LAUNCH(true, true, false);
-            else PHD_K1_LAUNCH(true, false, false);
-        }
-    } else {   // the statistics pass does not classify
-        if (aligned) PHD_K1_LAUNCH(false, true, true);
-        else PHD_K1_LAUNCH(false, false, true);
-    }
-#undef PHD_K1_LAUNCH
-    return hipGetLastError();
+    void* args[] = {(void*)&d_imgs, (void*)&npix, (void*)&nchunks, (void*)&nitems, (void*)&gp, (void*)&fc,
+                    (void*)&tabs, (void*)&k255, (void*)&out0, (void*)&a_stride, (void*)&h_stride,
+                    (void*)&cshift, nullptr};
+    const int abl = env_ablate();
+    args[12] = (void*)&abl;
+    return hipLaunchKernel(kfn, dim3(grid), dim3(kPalThreads), args, lds, st);
 }
 
 hipError_t launch_hsv_ds(const uint8_t* img, int height, int width, int ds, const GridParams& gp,
@@ -1196,7 +1401,15 @@ hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     bool aligned = true;
     for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
     const size_t lds = palette_sums_b_lds(gp.tl, max_slots);
-    const int grid = (int)std::min<long>(nitems, num_cus());
+    int per_cu = 0;
+    const void* kfn = fc.use_thr ? (aligned ? (const void*)k_palette_sums_b<true, true>
+                                            : (const void*)k_palette_sums_b<false, true>)
+                                 : (aligned ? (const void*)k_palette_sums_b<true, false>
+                                            : (const void*)k_palette_sums_b<false, false>);
+    (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kK3Threads, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
 #define PHD_K3_LAUNCH(A, T)                                                                                 \
     do {                                                                                                    \
         static bool attr = false;                                                                           \
@@ -1205,7 +1418,7 @@ hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              \
             attr = true;                                                                                    \
         }                                                                                                   \
-        hipLaunchKernelGGL((k_palette_sums_b<A, T>), dim3(grid), dim3(kK1Threads), lds, st, d_imgs, npix,        \
+        hipLaunchKernelGGL((k_palette_sums_b<A, T>), dim3(grid), dim3(kK3Threads), lds, st, d_imgs, npix,        \
                            nchunks, nitems, gp, fc, tabs, k255, rules0, off0, b_stride, nslots_img,         \
                            max_slots, out0, c_stride, k3_cshift(max_slots), env_ablate());                  \
     } while (0)
@@ -1217,6 +1430,36 @@ hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t
         else PHD_K3_LAUNCH(false, false);
     }
 #undef PHD_K3_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n,
+                                     int height, int width, const GridParams& gp, const FastCls& fc,
+                                     const ClassTables* tabs, const double* k255, const int2* entries,
+                                     int n_entries, const unsigned short* chunk_hist0, long h_stride,
+                                     const GroupRule* rules0, const double* off0, long b_stride, double* out0,
+                                     long c_stride, hipStream_t st) {
+    if (n_entries <= 0) return hipSuccess;
+    const long npix = (long)height * width;
+    bool aligned = true;
+    for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
+    const size_t lds = K1Lds::qn;
+    const dim3 grid(n_entries, 32);
+    if (fc.use_thr) {
+        if (aligned)
+            hipLaunchKernelGGL((k_partial_sums_b<true, true>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc,
+                               tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
+        else
+            hipLaunchKernelGGL((k_partial_sums_b<false, true>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
+                               fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
+    } else {
+        if (aligned)
+            hipLaunchKernelGGL((k_partial_sums_b<true, false>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
+                               fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
+        else
+            hipLaunchKernelGGL((k_partial_sums_b<false, false>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
+                               fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
+    }
     return hipGetLastError();
 }
 

@@ -61,6 +61,13 @@ Context* get_context() {
         return nullptr;
     }
     for (auto& e : c->ev) (void)hipEventCreate(&e);
+    if (hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_k1, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess) {
+        set_error("hipStreamCreate failed");
+        delete c;
+        return nullptr;
+    }
     g_ctx[dev] = c;
     return c;
 }

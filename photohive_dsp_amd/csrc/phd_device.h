@@ -126,6 +126,93 @@ __device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& 
     return (g & ~(mblack | mgray | medge)) | ((gp.tl - 1) & mblack) | (gray & mgray) | (-2 & medge);
 }
 
+// The fused K1's classification: classify_e() on the half-bin grid (cells of
+// Lh/2 = the wrap thresholds of calculate_avg_hsv, see HueCells) plus the
+// pixel's hue cell.  c = floor(2h / Lh) from the same exact integer form
+// (2N < 2^18 keeps the fp32 margin); the hue bin is c >> 1.  A non-special
+// pixel exactly on a half-bin boundary -- of any kind, grey and black
+// included, since its wrap side needs the reference's double -- returns -2
+// and is resolved after the stream (fused_exact).  A special pixel on a
+// boundary has the exact double hue B_c, which wraps for no parent whose
+// threshold is B_c: it goes to the side that never wraps (below for the
+// up-wrap thresholds B_c >= 180, above otherwise).  `cell` is the index into
+// the image's cell array (HueCells::cell_of).
+template <bool kThr>
+__device__ __forceinline__ int classify_f(int kr, int kg, int kb, const ClsEnt& e, const signed char* si8g,
+                                          const GridParams& gp, const FastCls& F, int& hN, int& hD,
+                                          int& cell) {
+    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
+    const int si = si_of<kThr>(e, kmx, kd, si8g);
+    const bool isr = kr == kmx, isg = kg == kmx;
+    const int a = isr ? kg : (isg ? kb : kr), b = isr ? kb : (isg ? kr : kg);
+    const int num = a - b;
+    const int base = isr ? (num < 0 ? 360 : 0) : (isg ? 120 : 240);
+    const int kd1 = max(kd, 1);
+    const int N = __mul24(base, kd1) + 60 * num, D = __mul24(F.lh, kd1);
+    hN = kd == 0 ? 0 : N;
+    hD = kd1;
+    const int c = (int)(((float)(2 * N) + 0.5f) * __builtin_amdgcn_rcpf((float)D));
+    const int hi = c >> 1;
+    const int special = (int)(num == 0) | (int)(num == kd) | (int)(num == -kd);
+    const int onb = (int)(__mul24(c, D) == 2 * N);
+    const int def = onb & (special ^ 1);
+    const int ch = c - gp.hp;
+    const int below = onb & special & (int)(ch >= 0) & ((ch & 1) | (int)(ch == 0));
+    const int vi = (e.vpack << 16) >> 16, gray = e.vpack >> 16;
+    const int g = __mul24(__mul24(hi, gp.sp) + si, gp.vp) + vi;
+    const int mblack = -(int)(vi < 0);
+    const int mgray = -(int)(si < 0) & ~mblack;
+    const int mdef = -def;
+    const int gg = (g & ~(mblack | mgray)) | ((gp.tl - 1) & mblack) | (gray & mgray);
+    const int gs = gp.tl - gp.ng - 1;
+    // colour group: 4 cells from the bin's lower edge; grey / black: 2*hp cells
+    const int cc = 4 * gg + 1 + (c & 1) - below;
+    const int cgray = 4 * gs + __mul24(gg - gs, 2 * gp.hp) + c - below;
+    const int cl = (mblack | mgray) ? cgray : cc;
+    cell = (cl & ~mdef) | ((4 * gs + (gp.ng + 1) * 2 * gp.hp) & mdef);
+    return (gg & ~mdef) | (-2 & mdef);
+}
+
+// The exact group and hue cell of a pixel classify_f() deferred (-2): its
+// rgb2hsv doubles, and on the boundary B_c the side calculate_avg_hsv's wrap
+// test puts it (src/color_quantization.c:538-546) for the one parent whose
+// threshold is B_c: up-wrap thresholds (B_c = hp_j + 180 or, for grey / black
+// parents, 180) go above when h + off > 360; down-wrap thresholds
+// (B_c = hp_j - 180) go below when h + off < 0.
+__device__ __forceinline__ int fused_exact(int kr, int kg, int kb, const double* k255, const GridParams& gp,
+                                           int lh, double& h, int& cell) {
+    double s, v;
+    rgb2hsv(k255[kr], k255[kg], k255[kb], h, s, v);
+    const int g = group_of(gp, h, s, v);
+    const int kmx = max(kr, max(kg, kb)), kd = kmx - min(kr, min(kg, kb));
+    const bool isr = kr == kmx, isg = kg == kmx;
+    const int num = isr ? kg - kb : (isg ? kb - kr : kr - kg);
+    const int base = isr ? (num < 0 ? 360 : 0) : (isg ? 120 : 240);
+    const int kd1 = max(kd, 1);
+    const int c = (2 * (base * kd1 + 60 * num)) / (lh * kd1);          // on the boundary: exact
+    const double B = (double)c * (double)lh * 0.5;                     // c * Lh / 2, exact
+    const int ch = c - gp.hp;
+    int below;
+    if (ch < 0) {
+        below = ((c + gp.hp) & 1) ? (int)((h + (-B)) < 0) : 0;         // off = 180 - hp_j = -B
+    } else if (ch == 0) {
+        below = (int)!((h + 180.0) > 360);                             // grey / black parent, off = 180
+    } else if (ch & 1) {
+        below = (int)!((h + (360.0 - B)) > 360);                       // off = 180 - hp_j = 360 - B
+    } else {
+        below = 0;
+    }
+    const int gs = gp.tl - gp.ng - 1;
+    const int cg = c - below;
+    if (g < gs) {
+        const int hi = g / (gp.sp * gp.vp);
+        cell = 4 * g + min(3, max(0, cg - 2 * hi + 1));
+    } else {
+        cell = 4 * gs + (g - gs) * 2 * gp.hp + cg;
+    }
+    return g;
+}
+
 template <bool kThr>
 __device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& e, const signed char* si8g,
                                           const GridParams& gp, const FastCls& F) {

@@ -111,6 +111,10 @@ struct Context {
     size_t ptrs_bytes = 0;
     size_t stage_bytes = 0;
     hipEvent_t ev[8] = {};
+    // the palette's second pass (rules upload, Kcut, sums) runs on its own
+    // stream, concurrent with the FFTs: joined by events
+    hipStream_t tail = nullptr;
+    hipEvent_t ev_k1 = nullptr, ev_tail = nullptr;
     KernelProfiler prof;
     std::mutex mu;
 };

@@ -53,6 +53,25 @@ struct PaletteDev {
     double* s_part;               // [nchunks] per-chunk sum of HSV saturation
     unsigned* hist;               // [TL] group quantities
     unsigned short* chunk_hist;   // [nchunks][TL]
+    double* gsum = nullptr;       // fused K1: [3][TL] sum h, sum s, sum v per group
+    unsigned* gcell = nullptr;    // fused K1: [HueCells::count] pixels per (group, hue cell)
+};
+
+// Hue cells of the fused palette pass.  calculate_avg_hsv
+// (src/color_quantization.c:527-547) adds off = 180 - h_parent to each hue and
+// wraps by 360 when the result leaves [0, 360]: with Lh = 360 / h_parts, the
+// thresholds h_parent +- 180 (and 180 for grey / black parents, h = 0) all
+// lie on the half-bin grid B_c = c * Lh / 2.  So the number of a group's
+// pixels that wrap for ANY parent is a sum of its counts per half-bin cell
+// [B_c, B_c+1).  A colour group (hue bin j) only holds hues in
+// [B_2j, B_2j+2]: 4 cells, global c = 2j - 1 + l; a grey or black group holds
+// any hue: 2 * h_parts cells.  Pixels exactly on a threshold are put on the
+// side the reference's double comparison puts them (classify_f / fused_exact).
+struct HueCells {
+    __host__ __device__ static int gray_start(const GridParams& g) { return g.tl - g.ng - 1; }
+    __host__ __device__ static int count(const GridParams& g) {
+        return 4 * gray_start(g) + (g.ng + 1) * 2 * g.hp;
+    }
 };
 
 // Keep rule of one octree group after group_irregular_pixels.
@@ -86,12 +105,24 @@ int num_cus();         // compute units of the current device
 // K1 over a batch of same-size images (ds == 1); d_imgs is a device array of
 // n image pointers; image i's records sit at out0 + i * a_stride (sums, hist,
 // s_part) and out0.chunk_hist + i * h_stride bytes.  hist == false computes
-// only the moments and sum(s) (the rgb2hsv + statistics pass).  aligned: every
-// image pointer is 4-byte aligned (word loads; else byte loads).
+// only the moments and sum(s) (the rgb2hsv + statistics pass).  sums (needs
+// hist and fused_palette_ok): also the per-group hsv sums and hue-cell counts
+// (out0.gsum / out0.gcell, every a_stride bytes).  aligned: every image
+// pointer is 4-byte aligned (word loads; else byte loads).
 hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width,
                                   const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
                                   const PaletteDev& out0, long a_stride, long h_stride, int nchunks,
-                                  const double* k255, bool hist, bool aligned, hipStream_t st);
+                                  const double* k255, bool hist, bool sums, bool aligned, hipStream_t st);
+// The fused K1's LDS fits this grid (else the palette uses K1 + K3).
+bool fused_palette_ok(const GridParams& gp);
+// Fused palette: the slot sums of the partial (tie-overflow) groups, added
+// into out0 (every c_stride bytes) after Kcut filled their cutoff / last.
+hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n,
+                                     int height, int width, const GridParams& gp, const FastCls& fc,
+                                     const ClassTables* tabs, const double* k255, const int2* entries,
+                                     int n_entries, const unsigned short* chunk_hist0, long h_stride,
+                                     const GroupRule* rules0, const double* off0, long b_stride, double* out0,
+                                     long c_stride, hipStream_t st);
 // Kcut and K3 over a batch (ds == 1): entries = (image, group) pairs needing a
 // cutoff search; B records (rules at rules0, slot offsets at off0) every
 // b_stride bytes; palette sums at out0 every c_stride bytes.  h_imgs: the same

@@ -30,7 +30,7 @@ size_t al(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 
 struct Layout {
     // per-image records
-    size_t a_sums, a_hist, a_spart, a_bytes;                 // read back after K1 (zeroed)
+    size_t a_sums, a_hist, a_spart, a_gsum, a_gcell, a_bytes;  // read back after K1 (zeroed)
     size_t c_bins, c_fmax, c_pal, c_sharp, c_bytes;         // read back at the end (zeroed)
     size_t b_rules, b_search, b_off, b_bytes;               // uploaded before K3
     size_t chunk_bytes;                                      // device only
@@ -47,12 +47,16 @@ struct Layout {
     size_t E_pin(int n) const { return P_pin(n) + ptr_bytes; }
 };
 
-Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolblocks) {
+// ncell > 0: the fused palette's per-group sums and hue-cell counts ride in
+// the K1 record.
+Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolblocks, int ncell = 0) {
     Layout L{};
     L.a_sums = 0;
     L.a_hist = al(6 * sizeof(unsigned long long));
     L.a_spart = L.a_hist + al(sizeof(unsigned) * tl);
-    L.a_bytes = L.a_spart + al(sizeof(double) * nchunks);
+    L.a_gsum = L.a_spart + al(sizeof(double) * nchunks);
+    L.a_gcell = L.a_gsum + (ncell > 0 ? al(sizeof(double) * 3 * tl) : 0);
+    L.a_bytes = L.a_gcell + (ncell > 0 ? al(sizeof(unsigned) * ncell) : 0);
     L.c_bins = 0;
     L.c_fmax = al(sizeof(double) * nbins);
     L.c_pal = L.c_fmax + al(sizeof(double) * (ncolblocks > 0 ? ncolblocks : 1));
@@ -232,7 +236,7 @@ bool all_aligned(const uint8_t* const* p, int n) {
 // K1 for n same-size images: one batched launch (ds == 1) over the device
 // pointer array staged in the workspace, or per-image launches (ds > 1).
 bool launch_k1(Context* c, const Layout& L, int n, const uint8_t* const* d_imgs, int height, int width, int ds,
-               const GridParams& gp, const Context::Cls* cls, int nchunks, hipStream_t st) {
+               const GridParams& gp, const Context::Cls* cls, int nchunks, bool fused, hipStream_t st) {
     uint8_t* dw = (uint8_t*)c->d_ws;
     uint8_t* hp = (uint8_t*)c->h_pin;
     PaletteDev pd;
@@ -240,13 +244,15 @@ bool launch_k1(Context* c, const Layout& L, int n, const uint8_t* const* d_imgs,
     pd.hist = (unsigned*)(dw + L.A(0) + L.a_hist);
     pd.s_part = (double*)(dw + L.A(0) + L.a_spart);
     pd.chunk_hist = (unsigned short*)(dw + L.H(n, 0));
+    pd.gsum = (double*)(dw + L.A(0) + L.a_gsum);
+    pd.gcell = (unsigned*)(dw + L.A(0) + L.a_gcell);
     const int ps = c->prof.begin(kK1, st);
     if (ds <= 1) {
         memcpy(hp + L.P_pin(n), d_imgs, sizeof(void*) * n);
         PHD_HIP(hipMemcpyAsync(dw + L.P_dev(n), hp + L.P_pin(n), sizeof(void*) * n, hipMemcpyHostToDevice, st));
         PHD_HIP(launch_hsv_stats_batch((const uint8_t* const*)(dw + L.P_dev(n)), n, height, width, gp, cls->fc,
                                        cls->d, pd, (long)L.a_bytes, (long)L.chunk_bytes, nchunks, c->d_k255,
-                                       true, all_aligned(d_imgs, n), st));
+                                       true, fused, all_aligned(d_imgs, n), st));
     } else {
         for (int i = 0; i < n; i++) {
             PaletteDev pi;
@@ -258,6 +264,58 @@ bool launch_k1(Context* c, const Layout& L, int n, const uint8_t* const* d_imgs,
         }
     }
     c->prof.end(ps, st);
+    return true;
+}
+
+// calculate_avg_hsv's slot sums (src/color_quantization.c:520-550) of every
+// group a slot keeps whole, from the fused K1's per-group records: sum over
+// the group of wrap(h + off) = sum(h) + n * off - 360 * #(h + off > 360)
+// + 360 * #(h + off < 0), the wrap counts being sums of hue-cell counts on
+// one side of the parent's threshold (HueCells).  Partial groups are left to
+// the device (k_partial_sums_b).  Adds into hs[4 * slot + {h, s, v, n}].
+bool fused_slot_sums(const GridParams& gp, const PaletteDecision& dec, const unsigned* hist, const double* gsum,
+                     const unsigned* gcell, double* hs, std::string* why) {
+    const int tl = gp.tl, gs = HueCells::gray_start(gp), hp = gp.hp, sv = gp.sp * gp.vp;
+    for (int g = 0; g < tl; g++) {
+        const GroupRule& r = dec.rules[g];
+        if (r.slot < 0 || r.partial || hist[g] == 0) continue;
+        const int k = r.slot, p = dec.parents[k];
+        // the parent's threshold cell cT and direction: +1 wraps down (-360)
+        // above cT, -1 wraps up (+360) below cT, 0 never
+        int cT = 0, dir = 0;
+        if (p >= gs) {
+            cT = hp;                                   // h = 0, off = 180: h > 180 wraps
+            dir = 1;
+        } else {
+            const int t = 2 * (p / sv) + 1;            // 2 * h_parent / Lh
+            if (t < hp) { cT = t + hp; dir = 1; }
+            else if (t > hp) { cT = t - hp; dir = -1; }
+        }
+        long long tot = 0, above = 0;
+        auto cell = [&](int cg, unsigned cnt) {
+            tot += cnt;
+            if (cg >= cT) above += cnt;
+        };
+        if (g < gs) {
+            const int hi = g / sv;
+            for (int l = 0; l < 4; l++) cell(std::max(0, 2 * hi - 1 + l), gcell[4 * g + l]);
+        } else {
+            for (int cg = 0; cg < 2 * hp; cg++) cell(cg, gcell[4 * gs + (g - gs) * 2 * hp + cg]);
+        }
+        if (tot != (long long)hist[g]) {
+            *why = "fused palette self-check failed: hue cells of group " + std::to_string(g) + " hold " +
+                   std::to_string(tot) + " pixels, the histogram " + std::to_string(hist[g]);
+            return false;
+        }
+        const double n = (double)hist[g];
+        double wrap = 0.0;
+        if (dir > 0) wrap = -360.0 * (double)above;
+        else if (dir < 0) wrap = 360.0 * (double)(tot - above);
+        hs[4 * k + 0] += gsum[g] + n * dec.off[k] + wrap;
+        hs[4 * k + 1] += gsum[tl + g];
+        hs[4 * k + 2] += gsum[2 * tl + g];
+        hs[4 * k + 3] += n;
+    }
     return true;
 }
 
@@ -281,6 +339,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         return false;
     }
     const hipStream_t st = stream ? stream : c->stream;
+    // a failed earlier call may have left second-pass work on the tail stream
+    PHD_HIP(hipStreamSynchronize(c->tail));
     const GridParams gp = make_grid(cfg);
     const GroupCenters gc = make_centers(gp);
     const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
@@ -296,7 +356,10 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (!tbl || !cls) return false;
 
     const int ncolblocks = fs.col_blocks;
-    const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks);
+    // fused palette (one pixel pass): ds == 1 and the fused K1's LDS fits; else K1 + K3
+    static const bool two_pass = getenv("PHD_PALETTE_TWO_PASS") != nullptr;
+    const bool fused = ds <= 1 && !two_pass && fused_palette_ok(gp);
+    const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks, fused ? HueCells::count(gp) : 0);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, sizeof(double2) * (size_t)(height + 1) * (wf + 1)))
         return false;
@@ -315,8 +378,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
 
     PHD_HIP(hipMemsetAsync(dw, 0, (size_t)n * (L.a_bytes + L.c_bytes), st));
     PHD_HIP(hipEventRecord(c->ev[0], st));
-    if (!launch_k1(c, L, n, d_imgs, height, width, ds, gp, cls, nchunks, st)) return false;
+    if (!launch_k1(c, L, n, d_imgs, height, width, ds, gp, cls, nchunks, fused, st)) return false;
     PHD_HIP(hipEventRecord(c->ev[1], st));
+    PHD_HIP(hipEventRecord(c->ev_k1, st));
     PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipEventRecord(c->ev[5], st));
     for (int i = 0; i < n; i++) {
@@ -343,6 +407,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipEventSynchronize(c->ev[5]));
     std::vector<PaletteDecision> dec(n);
     std::vector<int> ok(n, 1);
+    std::vector<std::vector<double>> hsum(n);                // fused: host part of the slot sums
     int* h_ent = (int*)(hp + L.E_pin(n) + L.e_entries);
     int* h_ns = (int*)(hp + L.E_pin(n) + L.e_ns);
     int n_ent = 0, max_slots = 1;
@@ -366,45 +431,71 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         }
         h_ns[i] = (int)dec[i].parents.size();
         max_slots = std::max(max_slots, h_ns[i]);
+        if (fused) {
+            hsum[i].assign(4 * dec[i].parents.size(), 0.0);
+            std::string w;
+            if (!fused_slot_sums(gp, dec[i], hist, (const double*)(hp + L.A(i) + L.a_gsum),
+                                 (const unsigned*)(hp + L.A(i) + L.a_gcell), hsum[i].data(), &w)) {
+                set_error(w);
+                ok[i] = 0;
+            }
+        }
     }
+    // the second pass on the tail stream, after K1, concurrent with the FFTs
+    const hipStream_t s2 = c->tail;
+    PHD_HIP(hipStreamWaitEvent(s2, c->ev_k1, 0));
     uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
-    PHD_HIP(hipMemcpyAsync(dw + L.B(n, 0), hb, (size_t)n * L.b_bytes, hipMemcpyHostToDevice, st));
-    const bool batched = ds <= 1 && palette_sums_b_lds(gp.tl, max_slots) <= 160 * 1024;
+    PHD_HIP(hipMemcpyAsync(dw + L.B(n, 0), hb, (size_t)n * L.b_bytes, hipMemcpyHostToDevice, s2));
+    const bool batched = ds <= 1 && (fused || palette_sums_b_lds(gp.tl, max_slots) <= 160 * 1024);
     if (batched) {
         // one Kcut and one K3 launch over the whole batch
-        PHD_HIP(hipMemcpyAsync(dw + L.E_dev(n), hp + L.E_pin(n), L.e_bytes, hipMemcpyHostToDevice, st));
+        PHD_HIP(hipMemcpyAsync(dw + L.E_dev(n), hp + L.E_pin(n), L.e_bytes, hipMemcpyHostToDevice, s2));
         const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(n));
-        int ps = n_ent ? c->prof.begin(kCutoffs, st) : -1;
+        int ps = n_ent ? c->prof.begin(kCutoffs, s2) : -1;
         PHD_HIP(launch_cutoffs_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
                                      (const int2*)(dw + L.E_dev(n) + L.e_entries), n_ent,
                                      (const unsigned short*)(dw + L.H(n, 0)), (long)L.chunk_bytes,
-                                     (GroupRule*)(dw + L.B(n, 0) + L.b_rules), (long)L.b_bytes, st));
-        c->prof.end(ps, st);
-        ps = c->prof.begin(kPalSums, st);
-        PHD_HIP(launch_palette_sums_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
-                                          (const GroupRule*)(dw + L.B(n, 0) + L.b_rules),
-                                          (const double*)(dw + L.B(n, 0) + L.b_off), (long)L.b_bytes,
-                                          (const int*)(dw + L.E_dev(n) + L.e_ns), max_slots,
-                                          (double*)(dw + L.C(n, 0) + L.c_pal), (long)L.c_bytes, st));
-        c->prof.end(ps, st);
+                                     (GroupRule*)(dw + L.B(n, 0) + L.b_rules), (long)L.b_bytes, s2));
+        c->prof.end(ps, s2);
+        if (fused) {
+            // only the partial groups' kept prefixes are left to sum on the device
+            ps = n_ent ? c->prof.begin(kPalSums, s2) : -1;
+            PHD_HIP(launch_partial_sums_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
+                                              (const int2*)(dw + L.E_dev(n) + L.e_entries), n_ent,
+                                              (const unsigned short*)(dw + L.H(n, 0)), (long)L.chunk_bytes,
+                                              (const GroupRule*)(dw + L.B(n, 0) + L.b_rules),
+                                              (const double*)(dw + L.B(n, 0) + L.b_off), (long)L.b_bytes,
+                                              (double*)(dw + L.C(n, 0) + L.c_pal), (long)L.c_bytes, s2));
+            c->prof.end(ps, s2);
+        } else {
+            ps = c->prof.begin(kPalSums, s2);
+            PHD_HIP(launch_palette_sums_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
+                                              (const GroupRule*)(dw + L.B(n, 0) + L.b_rules),
+                                              (const double*)(dw + L.B(n, 0) + L.b_off), (long)L.b_bytes,
+                                              (const int*)(dw + L.E_dev(n) + L.e_ns), max_slots,
+                                              (double*)(dw + L.C(n, 0) + L.c_pal), (long)L.c_bytes, s2));
+            c->prof.end(ps, s2);
+        }
     } else {
         for (int i = 0; i < n; i++) {
             if (!ok[i]) continue;
             GroupRule* rules = (GroupRule*)(dw + L.B(n, i) + L.b_rules);
             const int* search = (const int*)(dw + L.B(n, i) + L.b_search);
             const double* off = (const double*)(dw + L.B(n, i) + L.b_off);
-            int ps = dec[i].search.empty() ? -1 : c->prof.begin(kCutoffs, st);
+            int ps = dec[i].search.empty() ? -1 : c->prof.begin(kCutoffs, s2);
             PHD_HIP(launch_palette_cutoffs(d_imgs[i], height, width, ds, gp,
                                            (const unsigned short*)(dw + L.H(n, i)), nchunks, rules, search,
-                                           (int)dec[i].search.size(), c->d_k255, st));
-            c->prof.end(ps, st);
-            ps = c->prof.begin(kPalSums, st);
+                                           (int)dec[i].search.size(), c->d_k255, s2));
+            c->prof.end(ps, s2);
+            ps = c->prof.begin(kPalSums, s2);
             PHD_HIP(launch_palette_sums(d_imgs[i], height, width, ds, gp, rules, off,
                                         (int)dec[i].parents.size(), (double*)(dw + L.C(n, i) + L.c_pal),
-                                        c->d_k255, st));
-            c->prof.end(ps, st);
+                                        c->d_k255, s2));
+            c->prof.end(ps, s2);
         }
     }
+    PHD_HIP(hipEventRecord(c->ev_tail, s2));
+    PHD_HIP(hipStreamWaitEvent(st, c->ev_tail, 0));
     PHD_HIP(hipEventRecord(c->ev[3], st));
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
     PHD_HIP(hipMemcpyAsync(hc, dw + L.C(n, 0), (size_t)n * L.c_bytes, hipMemcpyDeviceToHost, st));
@@ -429,8 +520,13 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         const double* fpart = (const double*)(cc + L.c_fmax);
         double fmax = 0.0;
         for (int b = 0; b < ncolblocks; b++) fmax = fpart[b] > fmax ? fpart[b] : fmax;
+        const double* pal = (const double*)(cc + L.c_pal);
+        if (fused) {                                         // whole groups (host) + partial groups (device)
+            for (size_t k = 0; k < hsum[i].size(); k++) hsum[i][k] += pal[k];
+            pal = hsum[i].data();
+        }
         std::string w;
-        out[i] = assemble(st_i, s_acc / (double)n_hsv, dec[i], (const double*)(cc + L.c_pal), n_hsv, *tbl,
+        out[i] = assemble(st_i, s_acc / (double)n_hsv, dec[i], pal, n_hsv, *tbl,
                           (const double*)(cc + L.c_bins), fmax, cfg, crops,
                           (const double*)(cc + L.c_sharp), &w);
         if (!out[i]) {
@@ -473,7 +569,7 @@ bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, 
     pd.chunk_hist = (unsigned short*)(dw + L.H(1, 0));
     const Context::Cls* cls = get_cls(c, gp);
     if (!cls) return false;
-    if (!launch_k1(c, L, 1, &d_img, height, width, ds, gp, cls, nchunks, st)) return false;
+    if (!launch_k1(c, L, 1, &d_img, height, width, ds, gp, cls, nchunks, false, st)) return false;
     PHD_HIP(hipMemcpyAsync(hp, dw, L.a_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipStreamSynchronize(st));
     hist->assign((const unsigned*)(hp + L.a_hist), (const unsigned*)(hp + L.a_hist) + gp.tl);
@@ -716,7 +812,7 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
         return fail(e, "pointer upload");
     const int ps = c->prof.begin(kK1, st);
     if ((e = launch_hsv_stats_batch((const uint8_t* const*)(dw + rec), n_images, height, width, gp, cls->fc,
-                                    cls->d, pd, (long)a_stride, 0, nchunks, c->d_k255, false,
+                                    cls->d, pd, (long)a_stride, 0, nchunks, c->d_k255, false, false,
                                     all_aligned(hptr, n_images), st)) != hipSuccess)
         return fail(e, "launch");
     c->prof.end(ps, st);
@@ -860,6 +956,19 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
     pd.hist = (unsigned*)(dw + 256);
     pd.s_part = (double*)(dw + 256 + 4 * 4096);
     pd.chunk_hist = (unsigned short*)(dw + 256 + 4 * 4096 + 8 * (size_t)nchunks);
+    // K1 is timed as the report runs it: fused when the report fuses
+    const bool fused = ds <= 1 && getenv("PHD_PALETTE_TWO_PASS") == nullptr && fused_palette_ok(gp);
+    void* fscratch = nullptr;
+    if (fused) {
+        if (hipMalloc(&fscratch, sizeof(double) * 3 * gp.tl + sizeof(unsigned) * HueCells::count(gp)) != hipSuccess)
+            return -1;
+        pd.gsum = (double*)fscratch;
+        pd.gcell = (unsigned*)((double*)fscratch + 3 * gp.tl);
+    }
+    struct FreeOnExit {
+        void* p;
+        ~FreeOnExit() { if (p) (void)hipFree(p); }
+    } free_scratch{fscratch};
     const uint8_t** d_ptr = nullptr;
     if (!ensure_device((void**)&c->d_ptrs, &c->ptrs_bytes, sizeof(void*))) return -1;
     d_ptr = (const uint8_t**)c->d_ptrs;
@@ -875,7 +984,8 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
             case kNumKernels:   // K1 without the group histogram (the rgb2hsv + statistics pass)
                 e = ds > 1 ? launch_hsv_ds(d_rgb, height, width, ds, gp, cls->fc, cls->d, pd, nchunks, c->d_k255, st)
                            : launch_hsv_stats_batch(d_ptr, 1, height, width, gp, cls->fc, cls->d, pd, 0, 0, nchunks,
-                                                    c->d_k255, kernel == kK1, all_aligned(&d_rgb, 1), st);
+                                                    c->d_k255, kernel == kK1, kernel == kK1 && fused,
+                                                    all_aligned(&d_rgb, 1), st);
                 break;
             case kFftRows: e = launch_rows_sel(fs, d_rgb, height, width, pd.sums, c->d_k255, c->d_inter, st); break;
             case kFftCols: e = launch_cols_sel(fs, c->d_inter, height, wf, tbl->d_map,

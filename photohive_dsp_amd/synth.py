@@ -101,6 +101,14 @@ def grayish(h: int, w: int, seed: int) -> np.ndarray:
     return np.clip(out, 0, 255).astype(np.uint8)
 
 
+def posterized(h: int, w: int, seed: int, levels: int = 6) -> np.ndarray:
+    """Channels drawn from `levels` evenly spaced values (0, 51, ..., 255 for 6):
+    most hues are exact ratios, many of them on hue-bin edges and centres."""
+    step = 255 // (levels - 1)
+    u = splitmix64(seed, h * w * 3) % np.uint64(levels)
+    return (u.astype(np.int64) * step).astype(np.uint8).reshape(h, w, 3)
+
+
 def black(h: int, w: int, seed: int = 0) -> np.ndarray:
     return np.zeros((h, w, 3), dtype=np.uint8)
 
@@ -114,6 +122,7 @@ KINDS = {
     "dominant": dominant,
     "grayish": grayish,
     "black": black,
+    "posterized": posterized,
 }
 
 

@@ -255,6 +255,32 @@ def test_hsv_group_exhaustive_rgb_cube(cfg):
     np.testing.assert_array_equal(d_gid.cpu().numpy(), want)
 
 
+FUSED_CFGS = [{}, {"h_partitions": 9}, {"h_partitions": 15, "s_partitions": 3, "v_partitions": 2},
+              {"h_partitions": 5, "linked_list_size": 50}, {"h_partitions": 1, "s_partitions": 3},
+              {"h_partitions": 72, "s_partitions": 2, "v_partitions": 2, "linked_list_size": 64},
+              {"h_partitions": 36, "s_partitions": 4, "v_partitions": 5}, {"h_partitions": 360}]
+
+
+@pytest.mark.parametrize("kind", ["posterized", "uniform", "structured", "grayish"])
+@pytest.mark.parametrize("cfg", FUSED_CFGS, ids=lambda c: "_".join(f"{k[0]}{v}" for k, v in c.items()) or "default")
+def test_fused_palette_sums_against_oracle(cfg, kind):
+    """The one-pass palette (per-group sums + hue-cell wrap counts in K1, partial
+    groups on the device) against the oracle's per-pixel calculate_avg_hsv:
+    odd and even hue partitions put the wrap thresholds on bin centres or bin
+    edges; posterized images put many exact hues on them; small linked lists
+    make tie-overflow (partial) groups."""
+    phd, L, _ = _phd()
+    from photohive_dsp_amd import synth
+    from oracle import oracle as orc
+    img = synth.make(kind, 600, 800, 11)
+    rep = phd.get_report(img, **cfg)
+    o = orc.palette(img, **cfg)
+    cp = rep.color_palette
+    np.testing.assert_array_equal(np.array(cp.group_ids), o["valid_parents"])
+    np.testing.assert_array_equal(np.array(cp.quantities), o["palette_pct"])
+    np.testing.assert_allclose(np.array(cp.hsv).reshape(-1, 3), o["palette_hsv"], rtol=TIGHT_RTOL, atol=1e-12)
+
+
 @pytest.mark.parametrize("kind,seed", [("uniform", 5), ("structured", 6)])
 def test_power_spectrum_compile_time_fft_4000x3000(kind, seed):
     """The production FFT kernels' |X|^2 against numpy's rfft2 (pocketfft, fp64)

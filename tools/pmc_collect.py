@@ -45,7 +45,7 @@ def run_pass(counter, outdir, bench_args):
             if not k or row.get("Counter_Name") != counter:
                 continue
             per.setdefault(k, []).append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in per.items()}, files[0]
+    return {k: (sum(v) / len(v), len(v)) for k, v in per.items()}, files[0]
 
 
 def main():
@@ -59,13 +59,21 @@ def main():
     out = os.path.join(ROOT, "gpurun_out", "pmc")
     fetch, f1 = run_pass("FETCH_SIZE", out + "_fetch", bench_args)
     write, f2 = run_pass("WRITE_SIZE", out + "_write", bench_args)
+    sys.path.insert(0, ROOT)
+    from bench import parse as bench_parse
+    ba = bench_parse(bench_args)
+    images = ba.batch * (ba.steps + max(1, ba.warmup))     # every step, warmup included, is profiled
     res = {"image": f"{a.height}x{a.width}", "source": [os.path.relpath(f1, ROOT), os.path.relpath(f2, ROOT)],
+           "bench_args": bench_args,
            "correction": "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
-        fb, wb = fetch.get(k, 0.0) * 1024, write.get(k, 0.0) * 1024
-        res["kernels"][k] = {"fetch_size_kb": fetch.get(k), "write_size_kb": write.get(k),
-                             "hbm_bytes_per_launch": 2 * fb + wb}
+        (fk, n), (wk, _) = fetch.get(k, (0.0, 0)), write.get(k, (0.0, 0))
+        per_launch = images / max(n, 1)
+        hbm = 2 * fk * 1024 + wk * 1024
+        res["kernels"][k] = {"fetch_size_kb": fk, "write_size_kb": wk, "launches": n,
+                             "images_per_launch": per_launch, "hbm_bytes_per_launch": hbm,
+                             "hbm_bytes_per_image": hbm / per_launch}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     # profiles/ for bench.py on this box; gpurun_out/ is what travels back
     for d, name in ((os.path.join(ROOT, "profiles"), "pmc_latest.json"),
