@@ -17,7 +17,8 @@
 // Row kernel (persistent, 2 blocks per CU).  Each step handles one pair of
 // image rows.  Both rows' RGB8 bytes were prefetched into registers (dwordx3 =
 // 4 pixels) during the previous step.  They become luma - avg and are packed
-// as one complex row (row y0 real, row y0+1 imaginary) in LDS.  The next pair's
+// as one complex row (row y0 real, row y0+1 imaginary) in LDS (no DC removal:
+// the column pass does it on column 0, so the rows need nothing from K1).  The next pair's
 // loads are issued, then the FFT runs in LDS.  The two half spectra are
 // separated, A[k] = (Z[k] + conj Z[W-k]) / 2 and B[k] = (Z[k] - conj Z[W-k]) / 2i,
 // and stored as the pair's contiguous tile row.
@@ -58,7 +59,13 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // a native 128-bi
 
 constexpr double kWr = 0.299 / 255.0, kWg = 0.587 / 255.0, kWb = 0.114 / 255.0;
 
-__device__ __forceinline__ int byte_of(const unsigned (&w)[3], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255; }
+// 12 bytes (4 RGB8 pixels) as one dwordx3 register tuple; 4-byte alignment
+typedef unsigned u32x3a __attribute__((ext_vector_type(3), aligned(4)));
+
+__device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
+    const unsigned x = (b >> 2) == 0 ? w.x : ((b >> 2) == 1 ? w.y : w.z);   // b is a constant
+    return (x >> (8 * (b & 3))) & 255;
+}
 
 template <int W, int T, int... Rs>
 struct RowK {
@@ -82,10 +89,6 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
     double2* tw = buf + W;
     const int tid = threadIdx.x;
     for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
-    // avg = (Br + Bg + Bb) / 3 (src/interface.c:78) from the exact channel sums
-    const double n = (double)H * (double)W;
-    const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
-                        (double)sums[2] / 255.0 / n) / 3.0;
     // schedule: line group m (pairs 4m..4m+3) on XCD m % 8, its 4 pairs on 4
     // blocks of that XCD (gridDim.x is a multiple of 32)
     const int P = (H + 1) / 2;
@@ -93,28 +96,39 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
     const int a = q >> 2, i4 = q & 3;
     auto pair_of = [&](int s) { return 4 * (x + 8 * (a + s * QA)) + i4; };
 
-    unsigned rg[K::LR][2][3];
+    // the next pair's pixels, loaded straight into the registers the luma code
+    // reads (no moves, so nothing waits for the loads before they are used);
+    // groups past the row end re-load group 0 (unused, no branch)
+    u32x3a rg[K::LR][2];
     auto fetch = [&](int pr) {
+        // (byte addressing: a 3-vector's sizeof is 16, a group is 12 bytes)
         const int y0 = 2 * pr;
-        const unsigned* r0 = reinterpret_cast<const unsigned*>(img + (size_t)y0 * 3 * W);
-        const unsigned* r1 = (y0 + 1 < H) ? r0 + 3 * W / 4 : r0;
+        const uint8_t* r0 = img + (size_t)y0 * 3 * W;
+        const uint8_t* r1 = (y0 + 1 < H) ? r0 + 3 * W : r0;
 #pragma unroll
         for (int j = 0; j < K::LR; j++) {
-            const int g = tid + j * T;
-            if (K::G4 % T == 0 || g < K::G4) {
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    rg[j][0][c] = __builtin_nontemporal_load(r0 + 3 * g + c);
-                    rg[j][1][c] = __builtin_nontemporal_load(r1 + 3 * g + c);
-                }
-            }
+            const int g = (K::G4 % T == 0 || tid + j * T < K::G4) ? tid + j * T : 0;
+            rg[j][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x3a*>(r0 + 12 * g));
+            rg[j][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x3a*>(r1 + 12 * g));
         }
     };
     int s = 0, pr = pair_of(0);
     if (pr < P) fetch(pr);
     __syncthreads();
     const int rot = (tid >> 1) & 3;   // b128 write swizzle: 8 lanes of a group hit 8 distinct 16-B slots
-    while (pr < P) {
+    // one row pair.  The loop head is reached with the same memory operations in
+    // flight on every path (the prefetch, then the stores: a step's or, before
+    // the first step, as many dummy stores to a per-block slot), so the wait for
+    // the prefetched pixels counts the stores instead of draining them.
+    constexpr int WF_ = W / 2 + 1, KP_ = (WF_ + 1) / 2, NSO_ = (4 * KP_ + T - 1) / T;
+    {
+        // a scratch run just past the tiles (the intermediate has (H+1)(W/2+2) elements)
+        double2* slot = inter + (size_t)P * KP_ * 4 + (blockIdx.x & 63) * NSO_;
+#pragma unroll
+        for (int j = 0; j < NSO_; j++)
+            if ((4 * KP_) % T == 0 || tid + j * T < 4 * KP_) slot[j] = make_double2(0.0, 0.0);
+    }
+    auto step = [&]() __attribute__((always_inline)) {
         const int y0 = 2 * pr;
         const bool two = y0 + 1 < H;
 #pragma unroll
@@ -125,12 +139,12 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     // rgb2pgm (src/image_processing.c:509) with k/255 folded into the
-                    // weights (within 2 ulp), remove_dc_bias (src/blur_profile.c:236)
+                    // weights (within 2 ulp); remove_dc_bias is the column pass's
                     const double p0 = kWr * byte_of(rg[j][0], 3 * e) + kWg * byte_of(rg[j][0], 3 * e + 1) +
                                       kWb * byte_of(rg[j][0], 3 * e + 2);
                     const double p1 = kWr * byte_of(rg[j][1], 3 * e) + kWg * byte_of(rg[j][1], 3 * e + 1) +
                                       kWb * byte_of(rg[j][1], 3 * e + 2);
-                    z[e] = make_double2(p0 - avg, two ? p1 - avg : 0.0);
+                    z[e] = make_double2(p0, two ? p1 : 0.0);
                 }
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
@@ -139,27 +153,41 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
                 }
             }
         }
+        // unconditional (past the last pair it re-reads this one): every path into
+        // the loop head then has the same memory operations in flight
         const int prn = pair_of(s + 1);
-        if (prn < P && !(ablate & 4)) fetch(prn);
+        if (!(ablate & 4)) fetch(prn < P ? prn : pr);
         __syncthreads();
         if (!(ablate & 1)) fft_lds<W, T, 1, Rs...>(buf, tw, tid);
         constexpr int WF = W / 2 + 1, KP = (WF + 1) / 2;
         // the pair's tile row, contiguous: thread i -> (column pair i/4, column
         // k = 2(i/4) + (i/2)%2, row y0 + i%2); the phantom column WF (odd WF) is 0
+        // (a fixed, unrolled count per thread, branch-free: the next step's wait
+        // for its prefetched pixels can then count these stores exactly)
         double2* orow = inter + (size_t)pr * KP * 4;
-        for (int i = tid; i < 4 * KP && !(ablate & 2); i += T) {
-            const int k = 2 * (i >> 2) + ((i >> 1) & 1), second = i & 1;
-            const int kk = k < WF ? k : 0;
-            const double2 zk = buf[kk], zm = buf[kk == 0 ? 0 : W - kk];
-            double2 o = second ? make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x))
-                               : make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-            o = (k < WF && (two || !second)) ? o : make_double2(0.0, 0.0);
-            orow[i] = o;
+        constexpr int NSO = (4 * KP + T - 1) / T;
+#pragma unroll
+        for (int j = 0; j < NSO; j++) {
+            const int i = tid + j * T;
+            if ((4 * KP) % T == 0 || i < 4 * KP) {
+                if (ablate & 2) continue;
+                const int k = 2 * (i >> 2) + ((i >> 1) & 1);
+                const bool second = i & 1;
+                const int kk = k < WF ? k : 0;
+                const double2 zk = buf[kk], zm = buf[kk == 0 ? 0 : W - kk];
+                // first row: (Z[k] + conj Z[W-k]) / 2; second: (Z[k] - conj Z[W-k]) / 2i
+                const double ax = second ? zk.y : zk.x, bx = second ? zm.y : zm.x;
+                const double ay = second ? zk.x : zk.y, by = second ? zm.x : zm.y;
+                const bool keep = k < WF && (two || !second);
+                const double re = 0.5 * (ax + bx), im = (second ? -0.5 : 0.5) * (ay - by);
+                orow[i] = make_double2(keep ? re : 0.0, keep ? im : 0.0);
+            }
         }
         __syncthreads();
         s++;
         pr = prn;
-    }
+    };
+    while (pr < P) step();
 }
 
 // log(p) for p >= 1: e ln2 + log(m) with m = frexp mantissa and log(m) in fp32
@@ -194,8 +222,9 @@ template <int H, int T, int CPB, int... Rs>
 __global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) : 1) void k_cols_ct(const double2* __restrict__ inter, int wf,
                                                      const uint16_t* __restrict__ binmap, int nbins,
                                                      double* __restrict__ bin_sums, double* __restrict__ fmax_part,
-                                                     const double2* __restrict__ twg, double* __restrict__ dbg,
-                                                     int ablate_arg) {
+                                                     const double2* __restrict__ twg,
+                                                     const unsigned long long* __restrict__ sums, int width,
+                                                     double* __restrict__ dbg, int ablate_arg) {
     using K = ColK<H, T, CPB, Rs...>;
     const int ablate = PHD_ABL(ablate_arg);
     using L = typename K::L;
@@ -267,6 +296,19 @@ __global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 :
         }
         if (kp + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(kp + 1);
         __syncthreads();
+        if (kp == 0) {                                    // block-uniform
+            // remove_dc_bias (src/blur_profile.c:233-238): a constant per image only
+            // moves the row spectra's k = 0 column, by W * avg per row, with avg =
+            // (Br + Bg + Bb) / 3 (src/interface.c:78) from K1's exact channel sums
+            if (col == 0) {
+                const double n = (double)H * (double)width;
+                const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
+                                    (double)sums[2] / 255.0 / n) / 3.0;
+                const double dc = (double)width * avg;
+                for (int y = ht; y < H; y += T) buf[y].x -= dc;
+            }
+            __syncthreads();
+        }
         if (!(ablate & 1)) K::PL::all_but_last(buf, tw, ht);
         double2 v[L::ROUNDS][R];
         if (!(ablate & 16)) {
@@ -370,12 +412,12 @@ int cols_grid(int wf, int nbins) {
 }
 
 template <int H, int T, int CPB, int... Rs>
-hipError_t cols_ct(const double2* inter, int wf, const uint16_t* binmap, int nbins, double* bin_sums,
-                   double* fmax_part, const double2* tw, double* dbg, hipStream_t st) {
+hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binmap, int nbins, double* bin_sums,
+                   double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
+                   hipStream_t st) {
     const size_t lds = ColK<H, T, CPB, Rs...>::lds(nbins);
     hipLaunchKernelGGL((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3(CPB * T), lds,
-                       st, inter,
-                       wf, binmap, nbins, bin_sums, fmax_part, tw, dbg, g_ablate);
+                       st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, g_ablate);
     return hipGetLastError();
 }
 
@@ -455,12 +497,13 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_fft_cols_ct(const double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
-                              double* bin_sums, double* fmax_part, const double2* tw, double* dbg,
-                              hipStream_t st) {
+hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,
+                              int nbins, double* bin_sums, double* fmax_part, const double2* tw,
+                              const unsigned long long* sums, double* dbg, hipStream_t st) {
     const int n_ = height;
 #define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) return cols_ct<N, T, __VA_ARGS__>(inter, wf, binmap, nbins, bin_sums, fmax_part, tw, dbg, st);
+    if (n_ == N && V == v_) \
+        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, dbg, st);
     PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return hipErrorInvalidValue;

@@ -1300,6 +1300,9 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kPalThreads, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
+    // blocks per CU (PHD_K1_PER_CU caps it, for co-residency experiments with the row FFT)
+    static const int cap = getenv("PHD_K1_PER_CU") ? atoi(getenv("PHD_K1_PER_CU")) : 0;
+    if (cap > 0 && per_cu > cap) per_cu = cap;
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
     void* args[] = {(void*)&d_imgs, (void*)&npix, (void*)&nchunks, (void*)&nitems, (void*)&gp, (void*)&fc,
                     (void*)&tabs, (void*)&k255, (void*)&out0, (void*)&a_stride, (void*)&h_stride,

@@ -63,7 +63,10 @@ Context* get_context() {
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     if (hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_k1, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->fft, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ws, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fft, hipEventDisableTiming) != hipSuccess) {
         set_error("hipStreamCreate failed");
         delete c;
         return nullptr;
@@ -223,9 +226,12 @@ hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int 
                 : launch_fft_rows(img, height, width, s.prow->plan, sums, k255, inter, st);
 }
 
-hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int wf, const uint16_t* binmap,
-                           int nbins, double* bin_sums, double* fmax_part, double* dbg, hipStream_t st) {
-    if (s.ct) return launch_fft_cols_ct(inter, height, wf, binmap, nbins, bin_sums, fmax_part, s.tw_c, dbg, st);
+hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int width, int wf,
+                           const uint16_t* binmap, int nbins, double* bin_sums, double* fmax_part,
+                           const unsigned long long* sums, double* dbg, hipStream_t st) {
+    if (s.ct)
+        return launch_fft_cols_ct(inter, height, width, wf, binmap, nbins, bin_sums, fmax_part, s.tw_c, sums, dbg,
+                                  st);
     if (dbg) return hipErrorNotSupported;
     return launch_fft_cols(inter, height, wf, s.pcol->plan, binmap, nbins, bin_sums, fmax_part, st);
 }

@@ -115,6 +115,10 @@ struct Context {
     // stream, concurrent with the FFTs: joined by events
     hipStream_t tail = nullptr;
     hipEvent_t ev_k1 = nullptr, ev_tail = nullptr;
+    // the FFTs run on their own stream too: the compile-time row pass does not
+    // need K1, so it overlaps it (only the column pass waits for the sums)
+    hipStream_t fft = nullptr;
+    hipEvent_t ev_ws = nullptr, ev_fft = nullptr;
     KernelProfiler prof;
     std::mutex mu;
 };
@@ -139,8 +143,10 @@ struct FftSel {
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s);
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
                            const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st);
-hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int wf, const uint16_t* binmap,
-                           int nbins, double* bin_sums, double* fmax_part, double* dbg, hipStream_t st);
+// sums: K1's channel sums of the image (the compile-time column pass removes the DC bias)
+hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int width, int wf,
+                           const uint16_t* binmap, int nbins, double* bin_sums, double* fmax_part,
+                           const unsigned long long* sums, double* dbg, hipStream_t st);
 const BlurTable* get_table(Context* c, int height, int width, int nr, int na);
 // Classification tables of a grid (uploaded once per configuration).
 const Context::Cls* get_cls(Context* c, const GridParams& gp);

@@ -191,13 +191,15 @@ bool ct_cols_plan(int h, std::vector<int>* radices);
 size_t fft_cols_ct_lds(int height, int nbins);
 // persistent grid of the column kernel (= entries of fmax_part)
 int fft_cols_ct_blocks(int height, int wf, int nbins);
-// tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built)
+// tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built).
+// The row pass transforms the luma as is (sums unused): it does not wait for K1.
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
                               const double* k255, const double2* tw, double2* inter, hipStream_t st);
+// The column pass removes the DC bias (K1's channel sums) from column 0 first.
 // dbg (optional): the power spectrum, column-major [wf][height]
-hipError_t launch_fft_cols_ct(const double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
-                              double* bin_sums, double* fmax_part, const double2* tw, double* dbg,
-                              hipStream_t st);
+hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,
+                              int nbins, double* bin_sums, double* fmax_part, const double2* tw,
+                              const unsigned long long* sums, double* dbg, hipStream_t st);
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st);
 hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st);

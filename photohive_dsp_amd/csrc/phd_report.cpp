@@ -339,8 +339,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         return false;
     }
     const hipStream_t st = stream ? stream : c->stream;
-    // a failed earlier call may have left second-pass work on the tail stream
+    // a failed earlier call may have left work on the side streams
     PHD_HIP(hipStreamSynchronize(c->tail));
+    PHD_HIP(hipStreamSynchronize(c->fft));
     const GridParams gp = make_grid(cfg);
     const GroupCenters gc = make_centers(gp);
     const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
@@ -360,8 +361,15 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     static const bool two_pass = getenv("PHD_PALETTE_TWO_PASS") != nullptr;
     const bool fused = ds <= 1 && !two_pass && fused_palette_ok(gp);
     const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks, fused ? HueCells::count(gp) : 0);
+    // half-spectrum intermediates: one per image of a group of Q (the group's row
+    // passes run before its column passes; measured best at Q = 1)
+    // (+ 1024 elements of scratch past the tiles for the row pass's dummy stores)
+    const size_t inter_one = sizeof(double2) * ((size_t)(height + 1) * (wf + 1) + 1024);
+    static const int qcap = getenv("PHD_FFT_GROUP") ? atoi(getenv("PHD_FFT_GROUP")) : 0;
+    int Q = std::min(n, qcap > 0 ? qcap : 1);   // 1: the intermediate stays in the 256 MB MALL
+    while (Q > 1 && (size_t)Q * inter_one > ((size_t)2 << 30)) Q = (Q + 1) / 2;
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
-        !ensure_device((void**)&c->d_inter, &c->inter_bytes, sizeof(double2) * (size_t)(height + 1) * (wf + 1)))
+        !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)Q * inter_one))
         return false;
     uint8_t* dw = (uint8_t*)c->d_ws;
     uint8_t* hp = (uint8_t*)c->h_pin;
@@ -377,31 +385,48 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     }
 
     PHD_HIP(hipMemsetAsync(dw, 0, (size_t)n * (L.a_bytes + L.c_bytes), st));
+    PHD_HIP(hipEventRecord(c->ev_ws, st));
     PHD_HIP(hipEventRecord(c->ev[0], st));
     if (!launch_k1(c, L, n, d_imgs, height, width, ds, gp, cls, nchunks, fused, st)) return false;
     PHD_HIP(hipEventRecord(c->ev[1], st));
     PHD_HIP(hipEventRecord(c->ev_k1, st));
     PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipEventRecord(c->ev[5], st));
-    for (int i = 0; i < n; i++) {
-        const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
-        double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
-        double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
-        int ps = c->prof.begin(kFftRows, st);
-        PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255, c->d_inter, st));
-        c->prof.end(ps, st);
-        ps = c->prof.begin(kFftCols, st);
-        PHD_HIP(launch_cols_sel(fs, c->d_inter, height, wf, tbl->d_map, nbins, bins, fmx, nullptr, st));
-        c->prof.end(ps, st);
-        if (ncrops) {
-            // crop boxes: sharpness on the full-resolution luma before DC removal
-            PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
-                                     crop_arr.data() + ncrops, crop_arr.data() + 2 * ncrops,
-                                     crop_arr.data() + 3 * ncrops, c->d_k255,
-                                     (double*)(dw + L.C(n, i) + L.c_sharp), st));
+    // the FFTs on their stream: compile-time row passes start with K1, the
+    // column passes (DC removal) wait for it; runtime-plan rows need it too
+    const hipStream_t sf = c->fft;
+    PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
+    if (!fs.ct) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+    const size_t inter_elems = inter_one / sizeof(double2);
+    for (int g0 = 0; g0 < n; g0 += Q) {
+        const int g1 = std::min(n, g0 + Q);
+        for (int i = g0; i < g1; i++) {
+            const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+            const int ps = c->prof.begin(kFftRows, sf);
+            PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255,
+                                    c->d_inter + (size_t)(i - g0) * inter_elems, sf));
+            c->prof.end(ps, sf);
+        }
+        if (g0 == 0 && fs.ct) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+        for (int i = g0; i < g1; i++) {
+            const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+            double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
+            double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
+            const int ps = c->prof.begin(kFftCols, sf);
+            PHD_HIP(launch_cols_sel(fs, c->d_inter + (size_t)(i - g0) * inter_elems, height, width, wf, tbl->d_map,
+                                    nbins, bins, fmx, sums, nullptr, sf));
+            c->prof.end(ps, sf);
+            if (ncrops) {
+                // crop boxes: sharpness on the full-resolution luma before DC removal
+                PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
+                                         crop_arr.data() + ncrops, crop_arr.data() + 2 * ncrops,
+                                         crop_arr.data() + 3 * ncrops, c->d_k255,
+                                         (double*)(dw + L.C(n, i) + L.c_sharp), sf));
+            }
         }
     }
-    PHD_HIP(hipEventRecord(c->ev[2], st));
+    PHD_HIP(hipEventRecord(c->ev[2], sf));
+    PHD_HIP(hipEventRecord(c->ev_fft, sf));
 
     // host decisions while the FFTs run
     PHD_HIP(hipEventSynchronize(c->ev[5]));
@@ -496,6 +521,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     }
     PHD_HIP(hipEventRecord(c->ev_tail, s2));
     PHD_HIP(hipStreamWaitEvent(st, c->ev_tail, 0));
+    PHD_HIP(hipStreamWaitEvent(st, c->ev_fft, 0));
     PHD_HIP(hipEventRecord(c->ev[3], st));
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
     PHD_HIP(hipMemcpyAsync(hc, dw + L.C(n, 0), (size_t)n * L.c_bytes, hipMemcpyDeviceToHost, st));
@@ -988,9 +1014,9 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
                                                     all_aligned(&d_rgb, 1), st);
                 break;
             case kFftRows: e = launch_rows_sel(fs, d_rgb, height, width, pd.sums, c->d_k255, c->d_inter, st); break;
-            case kFftCols: e = launch_cols_sel(fs, c->d_inter, height, wf, tbl->d_map,
+            case kFftCols: e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map,
                                                cfg->radius_partitions * cfg->angle_partitions, (double*)pd.chunk_hist,
-                                               (double*)pd.chunk_hist + 65536, nullptr, st); break;
+                                               (double*)pd.chunk_hist + 65536, pd.sums, nullptr, st); break;
             default: set_error("kernel not supported by the timing hook"); g_ablate = 0; return -1;
         }
         if (e != hipSuccess) {
@@ -1043,7 +1069,8 @@ extern "C" int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int wi
     const hipStream_t st = c->stream;
     hipError_t e = launch_rows_sel(fs, d_rgb, height, width, (const unsigned long long*)dw, c->d_k255, c->d_inter, st);
     if (e == hipSuccess)
-        e = launch_cols_sel(fs, c->d_inter, height, wf, tbl->d_map, nbins, scratch, scratch + nbins, d_out, st);
+        e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map, nbins, scratch, scratch + nbins,
+                            (const unsigned long long*)dw, d_out, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(scratch);
     if (e != hipSuccess) {
