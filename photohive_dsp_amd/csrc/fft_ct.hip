@@ -204,12 +204,18 @@ struct ColK {
     static constexpr int R = Radices<Rs...>::count > 0 ? H / L::NB : 1;   // last radix
     static constexpr int NTW = tw_entries<1, Rs...>();
     static constexpr int P = (H + 1) / 2;                                 // row pairs
-    static constexpr int NT = CPB * T;                                    // block size
-    static constexpr int CR = (2 * CPB * P + NT - 1) / NT;                // prefetch rounds
+    // CPB = flags: bits 0-1 columns per block (1 or 2); 4: no register
+    // prefetch (the step's tiles are loaded at its start, other blocks of the
+    // CU hide the latency); 8: bins summed with global atomics (no LDS bins)
+    static constexpr int NC = CPB & 3;
+    static constexpr bool PF = !(CPB & 4);
+    static constexpr bool GB = (CPB & 8) != 0;
+    static constexpr int NT = NC * T;                                     // block size
+    static constexpr int CR = (2 * NC * P + NT - 1) / NT;                 // load rounds
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
-    static size_t lds(int nbins) { return sizeof(double2) * (CPB * H + NTW) + sizeof(double) * nbins; }
+    static size_t lds(int nbins) { return sizeof(double2) * (NC * H + NTW) + (GB ? 0 : sizeof(double) * nbins); }
     static_assert(Radices<Rs...>::product == H, "plan");
-    static_assert(CPB == 1 || CPB == 2, "columns per block");
+    static_assert(NC == 1 || NC == 2, "columns per block");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
 };
 
@@ -219,38 +225,41 @@ struct ColK {
 // into that XCD's L2 (the grid is a multiple of 16).
 // one-column blocks are sized for two resident blocks per CU
 template <int H, int T, int CPB, int... Rs>
-__global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) : 1) void k_cols_ct(const double2* __restrict__ inter, int wf,
+__global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) : 1) void k_cols_ct(const double2* __restrict__ inter, int wf,
                                                      const uint16_t* __restrict__ binmap, int nbins,
                                                      double* __restrict__ bin_sums, double* __restrict__ fmax_part,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums, int width,
                                                      double* __restrict__ dbg, int ablate_arg) {
     using K = ColK<H, T, CPB, Rs...>;
+    constexpr int NC = K::NC;
     const int ablate = PHD_ABL(ablate_arg);
     using L = typename K::L;
     constexpr int R = K::R, NT = K::NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* bufs = reinterpret_cast<double2*>(smem);         // [CPB][H]
-    double2* tw = bufs + CPB * H;
+    double2* tw = bufs + NC * H;
     double* lb = reinterpret_cast<double*>(tw + K::NTW);
     const int tid = threadIdx.x;
-    const int half = CPB == 2 ? (tid >= T ? 1 : 0) : (int)((blockIdx.x >> 3) & 1);   // column of the pair
-    const int ht = CPB == 2 ? tid - half * T : tid;
-    double2* buf = bufs + (CPB == 2 ? half * H : 0);
+    const int half = NC == 2 ? (tid >= T ? 1 : 0) : (int)((blockIdx.x >> 3) & 1);   // column of the pair
+    const int ht = NC == 2 ? tid - half * T : tid;
+    double2* buf = bufs + (NC == 2 ? half * H : 0);
     for (int i = tid; i < K::NTW; i += NT) tw[i] = twg[i];
-    for (int i = tid; i < nbins; i += NT) lb[i] = 0.0;
+    if (!K::GB)
+        for (int i = tid; i < nbins; i += NT) lb[i] = 0.0;
+    double* const bsum = K::GB ? bin_sums : lb;          // where the runs are added
     const int kpn = (wf + 1) / 2;
-    const int nlog = CPB == 2 ? (int)gridDim.x : (int)gridDim.x / 2;
-    const int lblk = CPB == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
+    const int nlog = NC == 2 ? (int)gridDim.x : (int)gridDim.x / 2;
+    const int lblk = NC == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
     const int c0 = (int)((long)lblk * kpn / nlog), c1 = (int)((long)(lblk + 1) * kpn / nlog);
-    // the tiles: element 4p + 2c + r is (row 2p + r, column 2kp + c).  CPB == 2
+    // the tiles: element 4p + 2c + r is (row 2p + r, column 2kp + c).  NC == 2
     // loads whole 64-B tiles (thread -> row pair tid/4, sub-element tid%4), CPB
     // == 1 its column's 32-B half (row pair tid/2, row tid%2)
-    constexpr int PER = 2 * CPB;                               // elements of one row pair a block loads
+    constexpr int PER = 2 * NC;                               // elements of one row pair a block loads
     // raw 16-byte words: the loads land in the registers the LDS stores read
     // (no moves, so nothing waits for them before the next step)
     u32x4 pf[K::CR];
-    const int prow0 = tid / PER, psub = CPB == 2 ? (tid & 3) : 2 * half + (tid & 1);
+    const int prow0 = tid / PER, psub = NC == 2 ? (tid & 3) : 2 * half + (tid & 1);
 #define PHD_COL_FETCH(kpv)                                                                  \
     do {                                                                                    \
         const u32x4* src_ = reinterpret_cast<const u32x4*>(inter) +                         \
@@ -261,12 +270,13 @@ __global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 :
             pf[c] = src_[(size_t)pr_ * kpn * 4];                                            \
         }                                                                                   \
     } while (0)
-    if (c0 < c1) PHD_COL_FETCH(c0);
+    if (K::PF && c0 < c1) PHD_COL_FETCH(c0);
     double mx = 0.0;
     __syncthreads();
     for (int kp = c0; kp < c1; kp++) {
+        if (!K::PF) PHD_COL_FETCH(kp);
         {
-            u32x4* dst = reinterpret_cast<u32x4*>(bufs + (CPB == 2 ? ((psub >> 1) & 1) * H : 0) + 2 * prow0 +
+            u32x4* dst = reinterpret_cast<u32x4*>(bufs + (NC == 2 ? ((psub >> 1) & 1) * H : 0) + 2 * prow0 +
                                                   (psub & 1));
 #pragma unroll
             for (int c = 0; c < K::CR; c++) {
@@ -294,7 +304,7 @@ __global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 :
                     bmw[j] = (unsigned)bcol[2 * j] | ((unsigned)bcol[2 * j + 1] << 16);
             }
         }
-        if (kp + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(kp + 1);
+        if (K::PF && kp + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(kp + 1);
         __syncthreads();
         if (kp == 0) {                                    // block-uniform
             // remove_dc_bias (src/blur_profile.c:233-238): a constant per image only
@@ -345,7 +355,7 @@ __global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 :
                     if (lg >= 0.0) {
                         const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
                         if (bin != cur) {
-                            if (cur >= 0) atomicAdd(&lb[cur], acc);
+                            if (cur >= 0) atomicAdd(&bsum[cur], acc);
                             cur = bin;
                             acc = 0.0;
                         }
@@ -353,7 +363,7 @@ __global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 :
                     }
                 }
             }
-            if (cur >= 0) atomicAdd(&lb[cur], acc);
+            if (cur >= 0) atomicAdd(&bsum[cur], acc);
         }
         __syncthreads();
     }
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(CPB * T, CPB == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 :
         for (int w = 0; w < (NT + 63) / 64; w++) m = fmax(m, red[w]);
         fmax_part[blockIdx.x] = m;
     }
-    for (int i = tid; i < nbins && !(ablate & 8); i += NT) {
+    for (int i = tid; i < nbins && !K::GB && !(ablate & 8); i += NT) {
         const double t = lb[i];
         if (t != 0.0) atomicAdd(&bin_sums[i], t);
     }
@@ -404,9 +414,9 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
 
 template <int H, int T, int CPB, int... Rs>
 int cols_grid(int wf, int nbins) {
-    int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, CPB * T, ColK<H, T, CPB, Rs...>::lds(nbins));
+    int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
     const int kpn = (wf + 1) / 2;
-    if (CPB == 2) return kpn < g ? kpn : g;
+    if ((CPB & 3) == 2) return kpn < g ? kpn : g;
     g = g / 16 * 16;                                        // XCD partner blocks b, b ^ 8
     return g < 16 ? 16 : g;
 }
@@ -416,7 +426,7 @@ hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binm
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st) {
     const size_t lds = ColK<H, T, CPB, Rs...>::lds(nbins);
-    hipLaunchKernelGGL((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3(CPB * T), lds,
+    hipLaunchKernelGGL((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3((CPB & 3) * T), lds,
                        st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, g_ablate);
     return hipGetLastError();
 }

@@ -171,19 +171,26 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 // PHD_CT_ROWS_VARIANT / PHD_CT_COLS_VARIANT select another for tuning runs.
 // The first radix is odd (LDS bank-conflict-free first pass, fft_engine.h).
 // Rows need length % 4 == 0.
+// rows: X(length, variant, threads, radices...).  Measured at 4000x3000:
+// v0 43.2 us, v1 43.7, v2 47.3 (25 16 10 at 400 threads), v3 47.3, v4 56.0
 #define PHD_CT_ROWS(X)              \
     X(4000, 0, 512, 5, 8, 10, 10)   \
     X(4000, 1, 256, 25, 16, 10)     \
-    X(4000, 2, 512, 25, 16, 10)     \
-    X(4000, 3, 512, 5, 10, 8, 10)
-// columns: X(length, variant, threads per column, columns per block, radices...)
+    X(4000, 2, 400, 25, 16, 10)     \
+    X(4000, 3, 256, 5, 8, 10, 10)   \
+    X(4000, 4, 384, 5, 8, 10, 10)
+// columns: X(length, variant, threads per column, flags, radices...); flags:
+// columns per block (1, 2) | 4 no register prefetch | 8 bins by global atomics.
+// Measured at 4000x3000 (tools/ct_sweep.py): v0 54.8 us, v2 55.5, v3 56.0,
+// v4 61.4, v5 61.2, v1 (2 columns, register prefetch, spills) 63.2; global
+// atomic bins 92-148 us (contention), so no variant uses them.
 #define PHD_CT_COLS(X)                 \
-    X(3000, 0, 384, 2, 5, 6, 10, 10)   \
-    X(3000, 1, 256, 1, 15, 20, 10)     \
-    X(3000, 2, 384, 1, 5, 6, 10, 10)   \
-    X(3000, 3, 512, 1, 5, 6, 10, 10)   \
-    X(3000, 4, 256, 2, 15, 20, 10)     \
-    X(3000, 5, 512, 2, 5, 6, 10, 10)
+    X(3000, 0, 256, 5, 15, 10, 20)     \
+    X(3000, 1, 384, 2, 5, 6, 10, 10)   \
+    X(3000, 2, 256, 5, 15, 20, 10)     \
+    X(3000, 3, 256, 5, 25, 12, 10)     \
+    X(3000, 4, 512, 5, 5, 6, 10, 10)   \
+    X(3000, 5, 300, 5, 5, 6, 10, 10)
 int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);

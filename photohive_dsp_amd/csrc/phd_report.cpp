@@ -394,9 +394,13 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipEventRecord(c->ev[5], st));
     // the FFTs on their stream: compile-time row passes start with K1, the
     // column passes (DC removal) wait for it; runtime-plan rows need it too
+    // (PHD_FFT_OVERLAP=1 lets the row passes start with K1; measured no faster,
+    // since K1's persistent blocks leave no room for them, and it blurs the
+    // per-kernel event timings, so by default the FFTs follow K1)
     const hipStream_t sf = c->fft;
+    static const bool overlap = getenv("PHD_FFT_OVERLAP") != nullptr;
     PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
-    if (!fs.ct) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+    if (!fs.ct || !overlap) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
     const size_t inter_elems = inter_one / sizeof(double2);
     for (int g0 = 0; g0 < n; g0 += Q) {
         const int g1 = std::min(n, g0 + Q);
