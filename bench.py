@@ -130,12 +130,12 @@ def main():
     lib.phd_profile_kernels(0 if dom is None else 1 << KERNELS.index(dom))
     barrier()
     t0 = time.perf_counter()
-    stage = [0.0] * 5
+    stage = [0.0] * 8
     for _ in range(args.steps):
         step()
-        tm = (ctypes.c_double * 5)()
-        lib.phd_last_timings(tm, 5)
-        for j in range(5):
+        tm = (ctypes.c_double * 8)()
+        lib.phd_last_timings(tm, 8)
+        for j in range(8):
             stage[j] += tm[j]
     torch.cuda.synchronize()
     barrier()
@@ -168,7 +168,8 @@ def main():
                    "global_batch": B * world, "image": f"{H}x{W}", "parallelism": f"images sharded over {world} GPU"},
         "stages_ms_per_step": {"hsv_stats": stage[0] / args.steps, "fft_rows_cols": stage[1] / args.steps,
                                "palette_pass2": stage[2] / args.steps, "gpu_total": stage[3] / args.steps,
-                               "host_total": stage[4] / args.steps},
+                               "host_total": stage[4] / args.steps, "host_enqueue": stage[5] / args.steps,
+                               "host_decisions": stage[6] / args.steps, "host_assembly": stage[7] / args.steps},
     }
     line["roofline"] = None
     if dom in kern:

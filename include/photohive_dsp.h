@@ -201,9 +201,11 @@ const char* phd_last_error(void);
 /* Device name / arch / CU count into buf; returns the HIP device ordinal or < 0. */
 int phd_device_info(char* buf, int buflen);
 
-/* Per-stage GPU timing of the most recent call on this thread (ms, from HIP
- * events on the library stream): [0] hsv+stats, [1] fft rows, [2] fft columns,
- * [3] palette pass 2, [4] whole call.  Returns the number of stages written. */
+/* Stage timing of the most recent report call (ms).  Device, from HIP events:
+ * [0] K1 (hsv + stats + palette sums), [1] FFT rows + columns, [2] palette
+ * pass 2 left after the FFTs, [3] whole device span.  Host wall clock: [4]
+ * whole call, [5] enqueue, [6] palette decisions + pass-2 enqueue, [7]
+ * report assembly.  Returns the number of stages written (<= n). */
 int phd_last_timings(double* ms, int n);
 
 /* Per-kernel GPU time from HIP events recorded on the launch stream around

@@ -433,7 +433,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipEventRecord(c->ev_fft, sf));
 
     // host decisions while the FFTs run
+    const auto t_enq = std::chrono::steady_clock::now();
     PHD_HIP(hipEventSynchronize(c->ev[5]));
+    const auto t_k1 = std::chrono::steady_clock::now();
     std::vector<PaletteDecision> dec(n);
     std::vector<int> ok(n, 1);
     std::vector<std::vector<double>> hsum(n);                // fused: host part of the slot sums
@@ -530,7 +532,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
     PHD_HIP(hipMemcpyAsync(hc, dw + L.C(n, 0), (size_t)n * L.c_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipEventRecord(c->ev[4], st));
+    const auto t_dec = std::chrono::steady_clock::now();
     PHD_HIP(hipEventSynchronize(c->ev[4]));
+    const auto t_sync = std::chrono::steady_clock::now();
     c->prof.collect();
 
     int failures = 0;
@@ -566,11 +570,17 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             status[i] = 0;
         }
     }
-    const double host_ms =
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
-    double tm[5] = {ms_between(c->ev[0], c->ev[1]), ms_between(c->ev[1], c->ev[2]),
-                    ms_between(c->ev[2], c->ev[3]), ms_between(c->ev[0], c->ev[4]), host_ms};
-    record_timings(tm, 5);
+    const auto t_end = std::chrono::steady_clock::now();
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    // device stages, then host: total, enqueue, decisions + pass-2 enqueue, assembly
+    // (a per-image D2H + assembly pipeline and a host thread pool were both
+    // measured slower: extra stream joins, thread wake-up latency)
+    double tm[8] = {ms_between(c->ev[0], c->ev[1]), ms_between(c->ev[1], c->ev[2]),
+                    ms_between(c->ev[2], c->ev[3]), ms_between(c->ev[0], c->ev[4]), ms(t_host0, t_end),
+                    ms(t_host0, t_enq), ms(t_k1, t_dec), ms(t_sync, t_end)};
+    record_timings(tm, 8);
     return failures == 0;
 }
 
