@@ -219,10 +219,10 @@ struct ColK {
     static_assert(T % 2 == 0, "threads cover whole row pairs");
 };
 
-// CPB == 2: one column pair per step; threads [0, T) take column 2kp, [T, 2T)
-// column 2kp+1.  CPB == 1: one column per block; blocks b and b ^ 8 (same XCD)
-// take the two columns of the same pairs, so each 64-byte tile is fetched once
-// into that XCD's L2 (the grid is a multiple of 16).
+// Two columns per block: one column pair per step; threads [0, T) take column
+// 2kp, [T, 2T) column 2kp+1.  One column per block: blocks b, b^8, b^16, b^24
+// (same XCD) take the four columns of the same 128-byte lines (two tiles), so
+// each line is fetched once into that XCD's L2 (the grid is a multiple of 32).
 // one-column blocks are sized for two resident blocks per CU
 template <int H, int T, int CPB, int... Rs>
 __global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) : 1) void k_cols_ct(const double2* __restrict__ inter, int wf,
@@ -241,7 +241,10 @@ __global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T 
     double2* tw = bufs + NC * H;
     double* lb = reinterpret_cast<double*>(tw + K::NTW);
     const int tid = threadIdx.x;
-    const int half = NC == 2 ? (tid >= T ? 1 : 0) : (int)((blockIdx.x >> 3) & 1);   // column of the pair
+    // NC == 1: blocks b, b^8, b^16, b^24 (one XCD) take the four columns of a
+    // 128-byte line (two tiles), so each line is fetched once into that L2
+    const int quad = NC == 2 ? 0 : (int)((blockIdx.x >> 3) & 3);
+    const int half = NC == 2 ? (tid >= T ? 1 : 0) : (quad & 1);   // column of the pair
     const int ht = NC == 2 ? tid - half * T : tid;
     double2* buf = bufs + (NC == 2 ? half * H : 0);
     for (int i = tid; i < K::NTW; i += NT) tw[i] = twg[i];
@@ -249,9 +252,13 @@ __global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T 
         for (int i = tid; i < nbins; i += NT) lb[i] = 0.0;
     double* const bsum = K::GB ? bin_sums : lb;          // where the runs are added
     const int kpn = (wf + 1) / 2;
-    const int nlog = NC == 2 ? (int)gridDim.x : (int)gridDim.x / 2;
-    const int lblk = NC == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
-    const int c0 = (int)((long)lblk * kpn / nlog), c1 = (int)((long)(lblk + 1) * kpn / nlog);
+    const int nunit = NC == 2 ? kpn : (kpn + 1) / 2;          // column pairs / tile pairs
+    const int nlog = NC == 2 ? (int)gridDim.x : (int)gridDim.x / 4;
+    const int lblk = NC == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
+    const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
+    // the column pair of step u (NC == 1: tile 2u or 2u+1; past the last tile
+    // the block re-reads the last one and idles)
+    auto pair_at = [&](int u) { return NC == 2 ? u : min(2 * u + (quad >> 1), kpn - 1); };
     // the tiles: element 4p + 2c + r is (row 2p + r, column 2kp + c).  NC == 2
     // loads whole 64-B tiles (thread -> row pair tid/4, sub-element tid%4), CPB
     // == 1 its column's 32-B half (row pair tid/2, row tid%2)
@@ -270,10 +277,11 @@ __global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T 
             pf[c] = src_[(size_t)pr_ * kpn * 4];                                            \
         }                                                                                   \
     } while (0)
-    if (K::PF && c0 < c1) PHD_COL_FETCH(c0);
+    if (K::PF && c0 < c1) PHD_COL_FETCH(pair_at(c0));
     double mx = 0.0;
     __syncthreads();
-    for (int kp = c0; kp < c1; kp++) {
+    for (int u = c0; u < c1; u++) {
+        const int kp = pair_at(u);
         if (!K::PF) PHD_COL_FETCH(kp);
         {
             u32x4* dst = reinterpret_cast<u32x4*>(bufs + (NC == 2 ? ((psub >> 1) & 1) * H : 0) + 2 * prow0 +
@@ -285,7 +293,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T 
                     dst[c * 2 * (NT / PER)] = pf[c];
             }
         }
-        const int col = 2 * kp + half;
+        const int col = NC == 2 ? 2 * kp + half : 2 * (2 * u + (quad >> 1)) + half;
         const bool live = col < wf;                       // the phantom column of an odd wf idles
         // bin ids of this thread's run of its column: u in [ht*E, ht*E + E).  The
         // table has 64 bytes of padding, so the last run may read past its end.
@@ -304,7 +312,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T 
                     bmw[j] = (unsigned)bcol[2 * j] | ((unsigned)bcol[2 * j + 1] << 16);
             }
         }
-        if (K::PF && kp + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(kp + 1);
+        if (K::PF && u + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(pair_at(u + 1));
         __syncthreads();
         if (kp == 0) {                                    // block-uniform
             // remove_dc_bias (src/blur_profile.c:233-238): a constant per image only
@@ -417,8 +425,8 @@ int cols_grid(int wf, int nbins) {
     int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
     const int kpn = (wf + 1) / 2;
     if ((CPB & 3) == 2) return kpn < g ? kpn : g;
-    g = g / 16 * 16;                                        // XCD partner blocks b, b ^ 8
-    return g < 16 ? 16 : g;
+    g = g / 32 * 32;                                        // XCD quads b, b^8, b^16, b^24
+    return g < 32 ? 32 : g;
 }
 
 template <int H, int T, int CPB, int... Rs>
