@@ -38,6 +38,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-events", action="store_true",
                    help="do not bracket kernels with HIP events (roofline then null)")
+    p.add_argument("--no-config3", action="store_true",
+                   help="skip the BASELINE config-3 line (512 x 1080p rgb2hsv + rgb_statistics pass)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                    help="per-kernel PMC traffic summary written by tools/pmc_collect.py")
     return p.parse_args(argv)
@@ -57,6 +59,46 @@ def cpu_baseline(h, w, n_images):
     return {"value": n_images / dt, "unit": "images/s", "cores": 1, "kind": "port",
             "sample": f"{n_images} x {h}x{w} uniform RGB8 full reports, oracle/phd_oracle.c -O2 "
                       f"+ scipy.fft.rfft2 (1 worker), {dt:.1f} s"}
+
+
+def config3(lib, last_error, n=512, h=1080, w=1920, iters=10):
+    """BASELINE config 3 (the HBM-roofline run): the rgb2hsv + rgb_statistics pass
+    (phd_hsv_stats_batch_device, stats.hip) over n device-resident 1080p images, one
+    launch per batch.  Kernel time from HIP events on the launch stream; algorithmic
+    bytes = 3 per pixel."""
+    import torch
+    from photohive_dsp_amd.structures import RGB_Statistics
+    nb = h * w * 3
+    t = torch.empty(n * nb, dtype=torch.uint8, device="cuda")
+    for i in range(n):
+        assert lib.phd_fill_uniform_device(t[i * nb:].data_ptr(), nb, i, None) == 0, last_error()
+    st = (RGB_Statistics * n)()
+    sat = (ctypes.c_double * n)()
+
+    def run():
+        if lib.phd_hsv_stats_batch_device(t.data_ptr(), n, h, w, 0, st, sat, None) != 0:
+            raise RuntimeError(f"hsv_stats batch failed: {last_error()}")
+    run()
+    lib.phd_profile_kernels(0)
+    lib.phd_profile_kernels(1)                      # K1 slot = the statistics pass
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        run()
+    wall = (time.perf_counter() - t0) / iters
+    tot, cnt = ctypes.c_double(), ctypes.c_long()
+    lib.phd_profile_read(0, ctypes.byref(tot), ctypes.byref(cnt))
+    lib.phd_profile_kernels(0)
+    us = 1000 * tot.value / max(cnt.value, 1)
+    ab = 3.0 * n * h * w
+    del t
+    torch.cuda.empty_cache()
+    return {"workload": f"{n} x {h}x{w} RGB8, rgb2hsv + rgb_statistics only, device-resident",
+            "images_per_s": round(n / wall, 1), "ms_per_batch_wall": round(1000 * wall, 3),
+            "roofline": {"kernel": "rgb_stats", "bound": "hbm", "achieved": round(ab / (us * 1e-6) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ab / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us, 2)}}
 
 
 def algorithmic_bytes(kernel, h, w):
@@ -191,6 +233,8 @@ def main():
                             "images_per_launch": per_launch,
                             "avg_launch_us": round(kern[dom]["avg_us"], 2)}
         line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
+    if not args.no_config3 and world == 1:
+        line["config3"] = config3(lib, last_error)
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(H, W, args.cpu_images)
     print(json.dumps(line), flush=True)

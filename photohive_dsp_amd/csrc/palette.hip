@@ -1282,6 +1282,9 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     const long npix = (long)height * width;
     const long nitems = (long)n * nchunks;
     if (sums && (!hist || !fused_palette_ok(gp))) return hipErrorInvalidValue;
+    // the statistics-only pass over word-aligned images: the lean kernel (stats.hip)
+    if (!hist && aligned && !getenv("PHD_STATS_K1"))
+        return launch_rgb_stats_batch(d_imgs, n, height, width, out0, a_stride, nchunks, st);
     const size_t lds = hsv_stats_lds(gp, hist, sums);
     const int cshift = sums ? k1_fused_cshift(gp) : k1_cshift(gp.tl);
     const void* kfn = nullptr;

@@ -113,6 +113,10 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
                                   const GridParams& gp, const FastCls& fc, const ClassTables* tabs,
                                   const PaletteDev& out0, long a_stride, long h_stride, int nchunks,
                                   const double* k255, bool hist, bool sums, bool aligned, hipStream_t st);
+// The rgb2hsv + statistics pass alone (moments and sum(s), no histogram) over
+// a batch of 4-byte-aligned images: stats.hip (out0.sums, out0.s_part).
+hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width, const PaletteDev& out0,
+                                  long a_stride, int nchunks, hipStream_t st);
 // The fused K1's LDS fits this grid (else the palette uses K1 + K3).
 bool fused_palette_ok(const GridParams& gp);
 // Fused palette: the slot sums of the partial (tie-overflow) groups, added

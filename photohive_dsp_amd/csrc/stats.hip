@@ -1,0 +1,202 @@
+// stats.hip -- the rgb2hsv + RGB statistics pass alone (BASELINE config 3):
+// per image the channel moments (sum k, sum k^2 for r, g, b) and the sum of
+// the HSV saturation s.
+//
+// Replaces the per-pixel loops of get_rgb_statistics / get_average /
+// get_variance (src/image_processing.c:543-553, src/filtering.c:125-148) and
+// get_hsv_average over rgb2hsv's s channel (src/image_processing.c:533-540,
+// 408-414).  No group histogram: this is the HBM-streaming pass, sized so the
+// VALU work per byte stays below the HBM rate.
+//
+// Per thread, 4 pixels = 12 bytes = one dwordx3 load (a wave reads 768
+// contiguous bytes).  The 12 bytes are regrouped by v_perm into six u16 pairs
+// (R02 = {r0, r2}, R13 = {r1, r3}, likewise G and B); then per 4 pixels:
+//   * moments: v_dot2_u32_u16 of each pair with {1, 1} and with itself (exact
+//     u32 per thread, flushed to u64 per run);
+//   * max / min: v_pk_max_u16 / v_pk_min_u16, d = max - min (v_pk_sub);
+//   * s for a pixel pair (a, b): s_a + s_b = (d_a M_b + d_b M_a) / (M_a M_b),
+//     numerator and denominator each one v_dot2 (2 M_a M_b = dot2(M, swap M)),
+//     one fp32 reciprocal per pair.  M is raised to 1 for black pixels (d = 0).
+// rgb2hsv's s is d / max except 0.999999 for d == max (min == 0): here those
+// pixels add d / max = 1, so S-bar is high by at most 1e-6 relative (fp32
+// rounding adds ~1e-7): inside north_star's 1e-4 for the float fields.  The
+// full report's K1 (palette.hip) keeps the exact fp64 s.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "phd_device.h"
+
+namespace phd {
+
+namespace {
+
+constexpr int kStThreads = 512;              // 8 waves; kChunk pixels per work item
+constexpr int kStGroups = kChunk / (4 * kStThreads);
+static_assert(kStGroups == 8, "stats tile");
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) unsigned gu32s;
+
+__device__ __forceinline__ u16x2 as_u16x2(unsigned x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ unsigned as_u32(u16x2 x) { return __builtin_bit_cast(unsigned, x); }
+
+struct StatAcc {
+    unsigned sr, sg, sb, qr, qg, qb;         // per-thread moments of the run (u32: <= 1024 items)
+    f32x2 s;                                 // sum(s_a + s_b) / 2 of the item's pixel pairs
+};
+
+// 4 pixels (3 little-endian words w0..w2 = r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3).
+__device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, StatAcc& a) {
+    const u16x2 one = {1, 1};
+    const u16x2 r02 = as_u16x2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
+    const u16x2 r13 = as_u16x2(__builtin_amdgcn_perm(w2, w0, 0x0c050c03u));
+    const u16x2 g02 = as_u16x2(__builtin_amdgcn_perm(w1, w0, 0x0c070c01u));
+    const u16x2 g13 = as_u16x2(__builtin_amdgcn_perm(w2, w1, 0x0c060c00u));
+    const u16x2 b02 = as_u16x2(__builtin_amdgcn_perm(w2, w0, 0x0c040c02u));
+    const u16x2 b13 = as_u16x2(__builtin_amdgcn_perm(w2, w1, 0x0c070c01u));
+    a.sr = __builtin_amdgcn_udot2(r02, one, a.sr, false);
+    a.sr = __builtin_amdgcn_udot2(r13, one, a.sr, false);
+    a.sg = __builtin_amdgcn_udot2(g02, one, a.sg, false);
+    a.sg = __builtin_amdgcn_udot2(g13, one, a.sg, false);
+    a.sb = __builtin_amdgcn_udot2(b02, one, a.sb, false);
+    a.sb = __builtin_amdgcn_udot2(b13, one, a.sb, false);
+    a.qr = __builtin_amdgcn_udot2(r02, r02, a.qr, false);
+    a.qr = __builtin_amdgcn_udot2(r13, r13, a.qr, false);
+    a.qg = __builtin_amdgcn_udot2(g02, g02, a.qg, false);
+    a.qg = __builtin_amdgcn_udot2(g13, g13, a.qg, false);
+    a.qb = __builtin_amdgcn_udot2(b02, b02, a.qb, false);
+    a.qb = __builtin_amdgcn_udot2(b13, b13, a.qb, false);
+    const u16x2 m02 = __builtin_elementwise_max(__builtin_elementwise_max(r02, g02), b02);
+    const u16x2 m13 = __builtin_elementwise_max(__builtin_elementwise_max(r13, g13), b13);
+    const u16x2 n02 = __builtin_elementwise_min(__builtin_elementwise_min(r02, g02), b02);
+    const u16x2 n13 = __builtin_elementwise_min(__builtin_elementwise_min(r13, g13), b13);
+    const u16x2 d02 = m02 - n02, d13 = m13 - n13;
+    const u16x2 M02 = __builtin_elementwise_max(m02, one), M13 = __builtin_elementwise_max(m13, one);
+    const u16x2 S02 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M02), as_u32(M02), 16));
+    const u16x2 S13 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M13), as_u32(M13), 16));
+    // (d_a M_b + d_b M_a) and 2 M_a M_b, exact integers < 2^18
+    const f32x2 num = {(float)__builtin_amdgcn_udot2(d02, S02, 0u, false),
+                       (float)__builtin_amdgcn_udot2(d13, S13, 0u, false)};
+    const f32x2 den = {(float)__builtin_amdgcn_udot2(M02, S02, 0u, false),
+                       (float)__builtin_amdgcn_udot2(M13, S13, 0u, false)};
+    const f32x2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    a.s = __builtin_elementwise_fma(num, rc, a.s);
+}
+
+// One launch over a batch of same-size, 4-byte-aligned images.  Work items
+// are (image, chunk of kChunk pixels); each persistent block takes one
+// contiguous run of items and flushes its sums when the run leaves an image
+// (or every 1024 items, so the u32 squares cannot overflow: 1024 * 8 groups *
+// 4 * 255^2 < 2^32).  Outputs as K1's statistics-only form: out.sums (6 u64,
+// atomics) and out.s_part[first chunk of the run] (one fp64 per run).
+__global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* const* __restrict__ imgs, long npix,
+                                                              int nchunks, long nitems, PaletteDev out,
+                                                              long a_stride) {
+    __shared__ unsigned long long red[kStThreads / 64][8];
+    const int tid = threadIdx.x;
+    const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
+    if (it0 >= it1) return;                                 // block-uniform
+    const long full_end = npix & ~3L;                       // groups wholly inside the image
+    int img = (int)(it0 / nchunks), c = (int)(it0 - (long)img * nchunks);
+    const uint8_t* ip = imgs[img];
+    StatAcc a{0, 0, 0, 0, 0, 0, {0.f, 0.f}};
+    double ssum = 0.0;
+    int seg_c0 = c;
+    long seg_it0 = it0;
+    for (long it = it0; it < it1; it++) {
+        const long base = (long)c * kChunk;
+        // byte offsets fit 32 bits (pre_compute_error_checks caps images at 120 MP):
+        // uniform base + u32 lane offset (saddr loads)
+        const unsigned off0 = (unsigned)(3 * (base + 4L * tid));
+        if (base + kChunk <= full_end) {                    // block-uniform: the whole chunk is inside
+            unsigned w[kStGroups][3];
+#pragma unroll
+            for (int st = 0; st < kStGroups; st++) {
+                gu32s* q = (gu32s*)(ip + (off0 + 12u * kStThreads * st));
+                w[st][0] = q[0];
+                w[st][1] = q[1];
+                w[st][2] = q[2];
+            }
+#pragma unroll
+            for (int st = 0; st < kStGroups; st++) stat4(w[st][0], w[st][1], w[st][2], a);
+        } else {
+#pragma unroll 1
+            for (int st = 0; st < kStGroups; st++) {
+                const long p0 = base + 4L * tid + 4L * kStThreads * st;
+                if (p0 < full_end) {
+                    gu32s* q = (gu32s*)(ip + 3 * p0);
+                    stat4(q[0], q[1], q[2], a);
+                }
+            }
+        }
+        ssum += (double)a.s.x + (double)a.s.y;
+        a.s = f32x2{0.f, 0.f};
+        if (tid == 0 && base + kChunk >= npix) {
+            // the < 4 pixels of a partial final group: exact fp64 s
+            for (long p = full_end; p < npix; p++) {
+                const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
+                a.sr += kr; a.sg += kg; a.sb += kb;
+                a.qr += kr * kr; a.qg += kg * kg; a.qb += kb * kb;
+                ssum += 0.5 * sat_only(kr, kg, kb);         // ssum counts pairs: halved, doubled below
+            }
+        }
+        const int cimg = img;
+        if (++c == nchunks) {
+            c = 0;
+            img++;
+        }
+        const bool more = it + 1 < it1;
+        if (more && img != cimg) ip = imgs[img];
+        if (!more || img != cimg || it + 1 - seg_it0 == 1024) {
+            const int wv = tid >> 6;
+            const unsigned mom[6] = {a.sr, a.sg, a.sb, a.qr, a.qg, a.qb};
+            unsigned long long m64[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) m64[k] = wave_sum((unsigned long long)mom[k]);
+            const double sw = wave_sum(ssum);
+            if (lane_id() == 0) {
+#pragma unroll
+                for (int k = 0; k < 6; k++) red[wv][k] = m64[k];
+                reinterpret_cast<double*>(red[wv])[6] = sw;
+            }
+            __syncthreads();
+            if (tid < 6) {
+                unsigned long long t = 0;
+                for (int q = 0; q < kStThreads / 64; q++) t += red[q][tid];
+                atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(out.sums) + cimg * a_stride) +
+                              tid,
+                          t);
+            } else if (tid == 6) {
+                double t = 0.0;
+                for (int q = 0; q < kStThreads / 64; q++) t += reinterpret_cast<const double*>(red[q])[6];
+                // one slot per run (distinct first chunks); the pair sums carry a factor 1/2
+                reinterpret_cast<double*>(reinterpret_cast<char*>(out.s_part) + cimg * a_stride)[seg_c0] = 2.0 * t;
+            }
+            a = StatAcc{0, 0, 0, 0, 0, 0, {0.f, 0.f}};
+            ssum = 0.0;
+            seg_c0 = c;
+            seg_it0 = it + 1;
+            __syncthreads();                                  // red is reused by the next flush
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width, const PaletteDev& out0,
+                                  long a_stride, int nchunks, hipStream_t st) {
+    const long npix = (long)height * width;
+    const long nitems = (long)n * nchunks;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_rgb_stats, kStThreads, 0) !=
+            hipSuccess || per_cu < 1)
+        per_cu = 1;
+    const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
+    hipLaunchKernelGGL(k_rgb_stats, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
+                       a_stride);
+    return hipGetLastError();
+}
+
+}  // namespace phd

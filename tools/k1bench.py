@@ -24,7 +24,7 @@ def k1_avg():
 
 
 tag = os.environ.get("PHD_LIB", "default")
-for n, h, w in [(64, 1080, 1920), (256, 1080, 1920)]:
+for n, h, w in [(64, 1080, 1920), (512, 1080, 1920)]:
     t = fill(n, h, w)
     st = (RGB_Statistics * n)()
     sat = (ctypes.c_double * n)()
