@@ -32,6 +32,7 @@ struct GridParams {
 struct FastCls {
     int lh;                    // Lh = 360 / h_partitions (integer division, :41)
     int use_thr;               // Si from ClsEnt::thr (s_partitions <= 6), else si8 in global memory
+    int k1t_cshift = -1;       // the table K1 (k1.hip) fits this grid with 1 << k1t_cshift copies
 };
 // Si is non-decreasing in kd = kmax - kmin for a fixed kmax (s = d / max is), so
 // it is -1 plus the number of thresholds kd reaches.
@@ -45,6 +46,14 @@ struct ClsEnt {                // per max channel value k (16 B: one LDS read pe
 struct ClassTables {           // device copy; ent is staged into LDS by the kernels
     ClsEnt ent[256];
     signed char si8[256 * 256];   // [kmax][kmax - kmin]: Si of s, -1 when s < gray_thresh
+    // the table K1 (k1.hip) classifies with: per (kmax, kd) a code (u8) for
+    // everything arm_octree decides without the hue -- black, the gray group, or
+    // the colour group's (Si, Vi) -- and per code its group / cell bases
+    unsigned char code8[256 * 256];
+    unsigned ce[256];             // bits 0-11: group of hue bin 0 (colour) or the group;
+                                  // 12-30: hue cell base; bit 31: colour
+    double inv[256];              // 1.0 / k (inv[0] = 0)
+    int codes_ok;                 // every (kmax, kd) got a code (sp * vp + ng + 1 <= 256)
 };
 
 // Per-image device workspace views used by the palette kernels.
@@ -100,6 +109,7 @@ struct FftPlan {
 
 // ---- launchers (kernels in *.hip) ------------------------------------------
 extern int g_ablate;   // ablation mask read by kernels under phd_debug_time_kernel
+int env_ablate();      // PHD_ABLATE (timing builds only)
 int num_cus();         // compute units of the current device
 // hsv/stats/histogram pass over one image (K1).  ds = downsample rate.
 // K1 over a batch of same-size images (ds == 1); d_imgs is a device array of
@@ -117,6 +127,13 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
 // a batch of 4-byte-aligned images: stats.hip (out0.sums, out0.s_part).
 hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width, const PaletteDev& out0,
                                   long a_stride, int nchunks, hipStream_t st);
+// The fused K1 of k1.hip (table classification, packed counts): cshift of its
+// lane-private copies, or -1 when this grid does not fit it (palette.hip's
+// fused K1 then runs).
+int k1t_cshift(const GridParams& gp, const ClassTables& host_tabs);
+hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int width, const GridParams& gp,
+                            const ClassTables* tabs, const PaletteDev& out0, long a_stride, long h_stride,
+                            int nchunks, const double* k255, int cshift, hipStream_t st);
 // The fused K1's LDS fits this grid (else the palette uses K1 + K3).
 bool fused_palette_ok(const GridParams& gp);
 // Fused palette: the slot sums of the partial (tie-overflow) groups, added

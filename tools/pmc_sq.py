@@ -23,7 +23,7 @@ PASSES = [
     ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64",
      "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"],
 ]
-NAMES = ["k_hsv_stats", "k_fft_rows", "k_fft_cols", "k_rows_ct", "k_cols_ct", "k_cutoffs", "k_palette_sums", "k_sharp"]
+NAMES = ["k_k1t", "k_rgb_stats", "k_hsv_stats", "k_fft_rows", "k_fft_cols", "k_rows_ct", "k_cols_ct", "k_cutoffs", "k_palette_sums", "k_sharp"]
 
 
 def main():
