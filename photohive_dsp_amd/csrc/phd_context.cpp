@@ -66,7 +66,12 @@ Context* get_context() {
         hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess ||
         hipStreamCreateWithFlags(&c->fft, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_ws, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fft, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_fft, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->fft2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rows[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rows[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_cols[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_cols[1], hipEventDisableTiming) != hipSuccess) {
         set_error("hipStreamCreate failed");
         delete c;
         return nullptr;

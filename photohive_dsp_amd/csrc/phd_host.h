@@ -119,6 +119,10 @@ struct Context {
     // need K1, so it overlaps it (only the column pass waits for the sums)
     hipStream_t fft = nullptr;
     hipEvent_t ev_ws = nullptr, ev_fft = nullptr;
+    // two-stream FFT pipeline: row passes on `fft`, column passes on `fft2`,
+    // ping-pong intermediates, so image i+1's rows overlap image i's columns
+    hipStream_t fft2 = nullptr;
+    hipEvent_t ev_rows[2] = {}, ev_cols[2] = {};
     KernelProfiler prof;
     std::mutex mu;
 };

@@ -342,6 +342,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // a failed earlier call may have left work on the side streams
     PHD_HIP(hipStreamSynchronize(c->tail));
     PHD_HIP(hipStreamSynchronize(c->fft));
+    PHD_HIP(hipStreamSynchronize(c->fft2));
     const GridParams gp = make_grid(cfg);
     const GroupCenters gc = make_centers(gp);
     const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
@@ -368,8 +369,14 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     static const int qcap = getenv("PHD_FFT_GROUP") ? atoi(getenv("PHD_FFT_GROUP")) : 0;
     int Q = std::min(n, qcap > 0 ? qcap : 1);   // 1: the intermediate stays in the 256 MB MALL
     while (Q > 1 && (size_t)Q * inter_one > ((size_t)2 << 30)) Q = (Q + 1) / 2;
+    // PHD_FFT_PIPE=1: a two-stream pipeline (rows of image i+1 beside the
+    // columns of image i, two intermediates).  Measured slower (5.2k vs 5.8k
+    // images/s at 4000x3000: the two 96 MB intermediates no longer share the
+    // MALL with the pixels), so the FFTs run serially on one stream by default.
+    static const bool pipe_env = getenv("PHD_FFT_PIPE") != nullptr;
+    const bool pipe = Q == 1 && n > 1 && pipe_env;
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
-        !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)Q * inter_one))
+        !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)(pipe ? 2 : Q) * inter_one))
         return false;
     uint8_t* dw = (uint8_t*)c->d_ws;
     uint8_t* hp = (uint8_t*)c->h_pin;
@@ -402,7 +409,34 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
     if (!fs.ct || !overlap) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
     const size_t inter_elems = inter_one / sizeof(double2);
-    for (int g0 = 0; g0 < n; g0 += Q) {
+    const hipStream_t sc = c->fft2;
+    if (pipe) {
+        PHD_HIP(hipStreamWaitEvent(sc, c->ev_k1, 0));            // DC removal needs K1's sums
+        for (int i = 0; i < n; i++) {
+            const int b = i & 1;
+            double2* inter = c->d_inter + (size_t)b * inter_elems;
+            const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+            if (i >= 2) PHD_HIP(hipStreamWaitEvent(sf, c->ev_cols[b], 0));   // image i-2's columns are done
+            int ps = c->prof.begin(kFftRows, sf);
+            PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255, inter, sf));
+            c->prof.end(ps, sf);
+            PHD_HIP(hipEventRecord(c->ev_rows[b], sf));
+            PHD_HIP(hipStreamWaitEvent(sc, c->ev_rows[b], 0));
+            double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
+            double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
+            ps = c->prof.begin(kFftCols, sc);
+            PHD_HIP(launch_cols_sel(fs, inter, height, width, wf, tbl->d_map, nbins, bins, fmx, sums, nullptr, sc));
+            c->prof.end(ps, sc);
+            if (ncrops) {
+                PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
+                                         crop_arr.data() + ncrops, crop_arr.data() + 2 * ncrops,
+                                         crop_arr.data() + 3 * ncrops, c->d_k255,
+                                         (double*)(dw + L.C(n, i) + L.c_sharp), sc));
+            }
+            PHD_HIP(hipEventRecord(c->ev_cols[b], sc));
+        }
+    }
+    for (int g0 = 0; g0 < (pipe ? 0 : n); g0 += Q) {
         const int g1 = std::min(n, g0 + Q);
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
@@ -429,8 +463,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             }
         }
     }
-    PHD_HIP(hipEventRecord(c->ev[2], sf));
-    PHD_HIP(hipEventRecord(c->ev_fft, sf));
+    // the last column pass ends the FFT work (it waited for the last row pass)
+    PHD_HIP(hipEventRecord(c->ev[2], pipe ? sc : sf));
+    PHD_HIP(hipEventRecord(c->ev_fft, pipe ? sc : sf));
 
     // host decisions while the FFTs run
     const auto t_enq = std::chrono::steady_clock::now();
