@@ -54,24 +54,24 @@ typedef const __attribute__((address_space(1))) unsigned gu32t;
 __device__ __forceinline__ u16x2 as2(unsigned x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ unsigned as1(u16x2 x) { return __builtin_bit_cast(unsigned, x); }
 
-// LDS carve (bytes); the variable part follows `var`.
-struct TLds {
-    static constexpr int code = 0;                        // 65536 u8
-    static constexpr int ce = 65536;                      // 256 u32
-    static constexpr int inv = ce + 1024;                 // 256 f64
-    static constexpr int red = inv + 2048;                // 16 waves x 8 x u64
-    static constexpr int var = red + 1024;
-};
+// LDS carve (bytes).  Every base a pixel touches (cells, h/s sums, the
+// reciprocals, the code tables) lies below 64 KiB, so it is a DS
+// instruction's immediate offset (no address add per access); the per-run
+// records and the queue follow the 64 KiB code table.
 constexpr int kQueue = 2048;                              // deferred-pixel queue (chunk offsets, u16)
-struct TVar {                                             // offsets of the variable part
-    int cells, gs2, rcell, cg, seg, r255, rmx, dq, qcnt, end;
+struct TVar {
+    int cells, gs2, ce, inv, red, code, rcell, cg, seg, r255, rmx, dq, qcnt, end;
 };
 __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     const int C = 1 << cshift;
     TVar v;
-    v.cells = TLds::var;                                            // (ncell+1) * C u64
+    v.cells = 0;                                                    // (ncell+1) * C u64
     v.gs2 = v.cells + 8 * (ncell + 1) * C;                          // (tl+1) * C * {h, s} f64
-    v.rcell = v.gs2 + 16 * (tl + 1) * C;                            // ncell u32
+    v.ce = v.gs2 + 16 * (tl + 1) * C;                               // 256 u32
+    v.inv = v.ce + 1024;                                            // 256 f64
+    v.red = v.inv + 2048;                                           // 16 waves x 8 x u64
+    v.code = v.red + 1024;                                          // 65536 u8
+    v.rcell = v.code + 65536;                                       // ncell u32
     v.cg = v.rcell + 4 * ncell;                                     // tl u32
     v.seg = v.cg + 4 * tl;                                          // tl u32
     v.r255 = v.seg + 4 * tl;                                        // tl u32
@@ -83,7 +83,7 @@ __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
 }
 
 struct TConst {
-    int lh, hp, spvp, ac, tl, gs, ncell, cshift, mycopy;
+    int lh, hp, spvp, ac, tl, gs, cgs, hp2, ncell, cshift, mycopy;
 };
 
 // The group of hue cell q (HueCells layout).
@@ -96,32 +96,48 @@ __device__ __forceinline__ int group_of_cell(int q, const TConst& X) {
 // Classify and count one pixel.  Returns true when the pixel is deferred
 // (a non-special hue on a half-bin boundary: fp64 after the chunk); its
 // count went to the dummy cell / group, which are never read.
-__device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, const unsigned char* code8,
-                                        const unsigned* ce, const double* inv, unsigned long long* cells,
-                                        double* gs2, const TConst& X, int abl) {
+struct TRead {
+    int code;
+    double ikd, imx;
+};
+// The pixel's three table reads (issued for a whole 4-pixel group before its
+// atomics: LDS operations complete in order, so a read placed after an atomic
+// would wait for it).
+__device__ __forceinline__ TRead t_read(int kmx, int kd, const unsigned char* __restrict__ code8,
+                                        const double* __restrict__ inv) {
+    return TRead{code8[(kmx << 8) | kd], inv[max(kd, 1)], inv[kmx]};
+}
+__device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, const TRead& rd,
+                                        unsigned long long* __restrict__ cells, double* __restrict__ gs2,
+                                        const TConst& X, int abl) {
+    const int kd1 = max(kd, 1);
+    const int code = rd.code;
+    const double ikd = rd.ikd, imx = rd.imx;
     const bool isr = kr == kmx, isg = kg == kmx;
     const int num = isr ? kg - kb : (isg ? kb - kr : kr - kg);
     const int t = isr ? (num < 0 ? 3 : 0) : (isg ? 1 : 2);     // base = 120 t
     // two channels equal <=> num is 0 or +-kd (rgb2hsv's hue is then exact)
     const bool special = (kr == kg) | (kg == kb) | (kr == kb);
-    const int kd1 = max(kd, 1);
     const int n2 = __mul24(240 * t, kd1) + 120 * num;            // 2N, N = base kd + 60 num
     const int D = __mul24(X.lh, kd1);
     const int c = (int)(((float)n2 + 0.5f) * __builtin_amdgcn_rcpf((float)D));
     const bool onb = __mul24(c, D) == n2;
-    const unsigned e = ce[code8[(kmx << 8) | kd]];
-    const int hie = (int)e < 0 ? (c >> 1) : 0;                 // hue bin, colour groups only
-    const int gg = __mul24(hie, X.spvp) + (int)(e & 0xFFFu);
+    const bool color = code < X.spvp;
+    const int hie = color ? (c >> 1) : 0;                       // hue bin, colour groups only
+    const int j = code - X.spvp;                                // gray / black: group - gray_start
+    const int gg = color ? __mul24(hie, X.spvp) + code : X.gs + j;
     const int ch = c - X.hp;
     const bool below = onb & special & (ch >= 0) & (((ch & 1) != 0) | (ch == 0));
-    const int cell = __mul24(hie, X.ac) + (int)((e >> 12) & 0x7FFFFu) + c - (int)below;
+    // colour: 4 gg + 1 + (c - 2 hi); gray / black: 4 gs + j 2 hp + c (HueCells)
+    const int cbase = color ? 4 * code + 1 + __mul24(hie, X.ac) : X.cgs + __mul24(j, X.hp2);
+    const int cell = cbase + c - (int)below;
     const bool def = onb & !special;
     const int gsel = def ? X.tl : gg, csel = def ? X.ncell : cell;
     const unsigned lo = 1u + ((unsigned)kmx << 16);
     const unsigned hi32 = (unsigned)(kmx + 1) & 256u;            // #(kmax == 255) at bit 40
     if (!(abl & 1)) atomicAdd(&cells[(csel << X.cshift) | X.mycopy], ((unsigned long long)hi32 << 32) | lo);
-    const double h = (double)(n2 >> 1) * inv[kd1];
-    const double s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * inv[kmx];
+    const double h = (double)(n2 >> 1) * ikd;
+    const double s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * imx;
     double* a = gs2 + 2 * ((gsel << X.cshift) | X.mycopy);
     if (!(abl & 2)) {
         atomicAdd(a, h);
@@ -139,7 +155,7 @@ __device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn
 // and the cell the side of B_c calculate_avg_hsv's wrap test puts h on, as
 // palette.hip's fused_exact.
 __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k255g, const GridParams& gp,
-                                        const unsigned char* code8, const unsigned* ce, const double* inv,
+                                        const unsigned char* code8, const double* inv,
                                         unsigned long long* cells, double* gs2, const TConst& X) {
     const double h = hue_exact(kr, kg, kb, k255g);
     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
@@ -156,15 +172,15 @@ __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k2
     else if (ch & 1) below = (int)!((h + (360.0 - B)) > 360);             // off = 360 - B
     else below = 0;
     const int cg = c - below;
-    const unsigned e = ce[code8[(kmx << 8) | kd]];
+    const int code = code8[(kmx << 8) | kd];
     int g, cell;
-    if ((int)e < 0) {
+    if (code < X.spvp) {
         const int hi = (int)(h / gp.Lh);
-        g = hi * X.spvp + (int)(e & 0xFFFu);
+        g = hi * X.spvp + code;
         cell = 4 * g + min(3, max(0, cg - 2 * hi + 1));
     } else {
-        g = (int)(e & 0xFFFu);
-        cell = (int)((e >> 12) & 0x7FFFFu) + cg;
+        g = X.gs + code - X.spvp;
+        cell = X.cgs + (code - X.spvp) * X.hp2 + cg;
     }
     const double s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * inv[kmx];
     const unsigned lo = 1u + ((unsigned)kmx << 16), hi32 = (unsigned)(kmx + 1) & 256u;
@@ -180,9 +196,10 @@ struct Mom {
 
 // 4 pixels: moments (packed), then each pixel classified; bit i of the
 // result = pixel i deferred.
-__device__ __forceinline__ unsigned t_group(unsigned w0, unsigned w1, unsigned w2, Mom& m, const unsigned char* code8,
-                                            const unsigned* ce, const double* inv, unsigned long long* cells,
-                                            double* gs2, const TConst& X, int abl) {
+__device__ __forceinline__ unsigned t_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
+                                            const unsigned char* __restrict__ code8, const double* __restrict__ inv,
+                                            unsigned long long* __restrict__ cells, double* __restrict__ gs2,
+                                            const TConst& X, int abl) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
     const u16x2 r13 = as2(__builtin_amdgcn_perm(w2, w0, 0x0c050c03u));
@@ -209,13 +226,20 @@ __device__ __forceinline__ unsigned t_group(unsigned w0, unsigned w1, unsigned w
     const unsigned R[2] = {as1(r02), as1(r13)}, G[2] = {as1(g02), as1(g13)}, B[2] = {as1(b02), as1(b13)};
     const unsigned Mx[2] = {M02, M13}, Mn[2] = {N02, N13};
     unsigned def = 0;
+    if (abl & 32) return 0;
+    TRead rd[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);               // pixel i: pair q, half i >> 1
+        const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF;
+        rd[i] = t_read(kmx, kmx - kmn, code8, inv);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int q = i & 1, sh = 16 * (i >> 1);
         const int kr = (R[q] >> sh) & 0xFFFF, kg = (G[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF;
-        if (abl & 32) continue;
-        def |= (unsigned)t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, code8, ce, inv, cells, gs2, X, abl) << i;
+        def |= (unsigned)t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, rd[i], cells, gs2, X, abl) << i;
     }
     return def;
 }
@@ -238,14 +262,15 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
     X.ac = 4 * X.spvp - 2;
     X.tl = gp.tl;
     X.gs = gp.tl - gp.ng - 1;
+    X.cgs = 4 * X.gs;
+    X.hp2 = 2 * gp.hp;
     X.ncell = HueCells::count(gp);
     X.cshift = cshift;
     X.mycopy = tid & cm;
     const TVar V = t_var(X.tl, X.ncell, cshift);
-    unsigned char* code8 = smem + TLds::code;
-    unsigned* ce = reinterpret_cast<unsigned*>(smem + TLds::ce);
-    double* inv = reinterpret_cast<double*>(smem + TLds::inv);
-    unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + TLds::red);
+    unsigned char* code8 = smem + V.code;
+    double* inv = reinterpret_cast<double*>(smem + V.inv);
+    unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + V.red);
     unsigned long long* cells = reinterpret_cast<unsigned long long*>(smem + V.cells);
     double* gs2 = reinterpret_cast<double*>(smem + V.gs2);
     unsigned* rcell = reinterpret_cast<unsigned*>(smem + V.rcell);
@@ -259,20 +284,16 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
         const uint4* src = reinterpret_cast<const uint4*>(tabs->code8);
         uint4* dst = reinterpret_cast<uint4*>(code8);
         for (int i = tid; i < 65536 / 16; i += kT) dst[i] = src[i];
-        for (int i = tid; i < 256; i += kT) {
-            ce[i] = tabs->ce[i];
-            inv[i] = tabs->inv[i];
-        }
-        unsigned* z = reinterpret_cast<unsigned*>(smem + V.cells);
-        for (int i = tid; i < (V.end - V.cells) / 4; i += kT) z[i] = 0u;
+        for (int i = tid; i < 256; i += kT) inv[i] = tabs->inv[i];
+        unsigned* z = reinterpret_cast<unsigned*>(smem);
+        for (int i = tid; i < V.ce / 4; i += kT) z[i] = 0u;                        // cells, h/s sums
+        for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;         // run records, queue
     }
     const int ng1 = (X.tl + 1) * C;
-    // the (0, 0, 0) pixel's cell: masked groups past the image end are zero pixels
-    int zcell;
-    {
-        const unsigned e0 = tabs->ce[tabs->code8[0]];
-        zcell = (int)((e0 >> 12) & 0x7FFFFu);                  // c = 0, hue bin 0, not below
-    }
+    // the (0, 0, 0) pixel's cell: masked groups past the image end are zero
+    // pixels (c = 0, hue bin 0, not below)
+    const int code0 = tabs->code8[0];
+    const int zcell = code0 < X.spvp ? 4 * code0 + 1 : X.cgs + (code0 - X.spvp) * X.hp2;
     __syncthreads();
 
     const long full_end = npix & ~3L;
@@ -322,7 +343,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
         unsigned emask = 0;                                       // deferred pixels (bit 4 st + i)
 #pragma unroll
         for (int st = 0; st < kG; st++)
-            emask |= t_group(cw[st][0], cw[st][1], cw[st][2], m, code8, ce, inv, cells, gs2, X, abl) << (4 * st);
+            emask |= t_group(cw[st][0], cw[st][1], cw[st][2], m, code8, inv, cells, gs2, X, abl) << (4 * st);
         if (abl & 4) emask = 0;
         const bool last_chunk = base + kChunk >= npix;            // block-uniform
         if (last_chunk && tid == 0) {
@@ -332,8 +353,8 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
                 m.sr += kr; m.sg += kg; m.sb += kb;
                 m.qr += kr * kr; m.qg += kg * kg; m.qb += kb * kb;
                 const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
-                if (t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, code8, ce, inv, cells, gs2, X, 0))
-                    t_exact(kr, kg, kb, k255g, gp, code8, ce, inv, cells, gs2, X);
+                if (t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, t_read(kmx, kmx - kmn, code8, inv), cells, gs2, X, 0))
+                    t_exact(kr, kg, kb, k255g, gp, code8, inv, cells, gs2, X);
             }
         }
         // deferred pixels: queued in LDS (chunk offsets) and resolved by all
@@ -349,7 +370,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
                     dq[pos++] = (unsigned short)off;
                 } else {
                     const long p = base + off;
-                    t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255g, gp, code8, ce, inv, cells, gs2, X);
+                    t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255g, gp, code8, inv, cells, gs2, X);
                 }
             }
         }
@@ -360,7 +381,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
         if (nq > 0) {
             for (int i = tid; i < nq; i += kT) {
                 const long p = base + dq[i];
-                t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255g, gp, code8, ce, inv, cells, gs2, X);
+                t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255g, gp, code8, inv, cells, gs2, X);
             }
             __syncthreads();
         }

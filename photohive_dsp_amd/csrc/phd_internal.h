@@ -46,12 +46,11 @@ struct ClsEnt {                // per max channel value k (16 B: one LDS read pe
 struct ClassTables {           // device copy; ent is staged into LDS by the kernels
     ClsEnt ent[256];
     signed char si8[256 * 256];   // [kmax][kmax - kmin]: Si of s, -1 when s < gray_thresh
-    // the table K1 (k1.hip) classifies with: per (kmax, kd) a code (u8) for
-    // everything arm_octree decides without the hue -- black, the gray group, or
-    // the colour group's (Si, Vi) -- and per code its group / cell bases
+    // the table K1 (k1.hip) classifies with: per (kmax, kd <= kmax) a code
+    // (u8) for everything arm_octree decides without the hue -- the colour
+    // group's (Si, Vi) as Si * vp + Vi, else sp * vp + (gray / black group -
+    // gray_start)
     unsigned char code8[256 * 256];
-    unsigned ce[256];             // bits 0-11: group of hue bin 0 (colour) or the group;
-                                  // 12-30: hue cell base; bit 31: colour
     double inv[256];              // 1.0 / k (inv[0] = 0)
     int codes_ok;                 // every (kmax, kd) got a code (sp * vp + ng + 1 <= 256)
 };

@@ -120,40 +120,22 @@ void make_class_tables(const GridParams& g, FastCls* fc, ClassTables* t) {
             t->ent[k].thr[i] = (unsigned)thr[2 * i] | ((unsigned)thr[2 * i + 1] << 16);
     }
     fc->use_thr = mono ? 1 : 0;
-    // K1 table: code per (kmax, kd); codes 0..sp*vp-1 colour (Si * vp + Vi),
-    // then the gray / black groups by id (only the ones that occur)
+    // K1 table (k1.hip): a code per (kmax, kd <= kmax): 0 .. sp*vp-1 colour
+    // (Si * vp + Vi), sp*vp + (group - gray_start) for the gray / black groups
     const int gs = g.tl - g.ng - 1, sv = g.sp * g.vp;
-    int ncode = sv;
-    int code_of_group[4096];
-    for (int i = 0; i < 4096; i++) code_of_group[i] = -1;
-    t->codes_ok = 1;
-    for (int k = 0; k < 256; k++) {
+    t->codes_ok = sv + g.ng + 1 <= 256 && g.tl <= 4095;
+    for (int k = 0; k < 256 && t->codes_ok; k++) {
         const int vcol = (int)(short)(t->ent[k].vpack & 0xFFFF), gray_id = (int)((unsigned)t->ent[k].vpack >> 16);
-        for (int kd = 0; kd < 256; kd++) {
-            int code = 0;
-            if (kd <= k) {
-                const int si = t->si8[k * 256 + kd];
-                int grp = -1;
-                if (vcol < 0) grp = g.tl - 1;               // black (v < bt)
-                else if (si < 0) grp = gray_id;             // gray (s < gt)
-                if (grp < 0) {
-                    code = si * g.vp + vcol;
-                } else {
-                    if (grp >= 4096 || grp < gs) { t->codes_ok = 0; continue; }
-                    if (code_of_group[grp] < 0) {
-                        if (ncode >= 256) { t->codes_ok = 0; continue; }
-                        code_of_group[grp] = ncode;
-                        t->ce[ncode] = (unsigned)grp | ((unsigned)(4 * gs + (grp - gs) * 2 * g.hp) << 12);
-                        ncode++;
-                    }
-                    code = code_of_group[grp];
-                }
-            }
+        for (int kd = 0; kd <= k; kd++) {
+            const int si = t->si8[k * 256 + kd];
+            int code;
+            if (vcol < 0) code = sv + (g.tl - 1 - gs);              // black (v < bt)
+            else if (si < 0) code = sv + (gray_id - gs);            // gray (s < gt)
+            else code = si * g.vp + vcol;
+            if (code < 0 || code > 255) t->codes_ok = 0;
             t->code8[k * 256 + kd] = (unsigned char)code;
         }
     }
-    for (int c = 0; c < sv; c++) t->ce[c] = (unsigned)c | ((unsigned)(4 * c + 1) << 12) | 0x80000000u;
-    if (g.tl > 4095 || 4 * gs + (g.ng + 1) * 2 * g.hp >= (1 << 19)) t->codes_ok = 0;
     t->inv[0] = 0.0;
     for (int k = 1; k < 256; k++) t->inv[k] = 1.0 / (double)k;
     fc->k1t_cshift = k1t_cshift(g, *t);
