@@ -68,6 +68,7 @@ Context* get_context() {
         hipEventCreateWithFlags(&c->ev_ws, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fft, hipEventDisableTiming) != hipSuccess ||
         hipStreamCreateWithFlags(&c->fft2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->dl, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rows[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rows[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_cols[0], hipEventDisableTiming) != hipSuccess ||

@@ -123,6 +123,11 @@ struct Context {
     // ping-pong intermediates, so image i+1's rows overlap image i's columns
     hipStream_t fft2 = nullptr;
     hipEvent_t ev_rows[2] = {}, ev_cols[2] = {};
+    // per-image download: image i's C record leaves on `dl` as soon as its
+    // column pass (ev_img_fft[i]) and the palette tail are done, so the host
+    // assembles image i while the FFTs of the later images run
+    hipStream_t dl = nullptr;
+    std::vector<hipEvent_t> ev_img_fft, ev_img_dl;
     KernelProfiler prof;
     std::mutex mu;
 };

@@ -168,23 +168,25 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
     bp->num_radius_bins = nr;
     bp->angle_bin_size = tbl.angle_bin_size;
     bp->radius_bin_size = tbl.radius_bin_size;
+    // bins[angle][radius] as the reference's row pointers, the rows in one
+    // block (free_full_report frees bins[0] and the pointer array)
     bp->bins = (Bin**)malloc(sizeof(Bin*) * na);
+    Bin* rows = (Bin*)calloc((size_t)na * nr > 0 ? (size_t)na * nr : 1, sizeof(Bin));
     const double gs = 1 / (2 * std::log(std::sqrt(fmax) + 1));
-    std::vector<double> flat((size_t)na * nr);
     for (int a = 0; a < na; a++) {
-        bp->bins[a] = (Bin*)calloc(nr, sizeof(Bin));
+        bp->bins[a] = rows + (size_t)a * nr;
         for (int r = 0; r < nr; r++) {
             const size_t b = (size_t)a * nr + r;
             const double q = (double)tbl.counts[b];
             const double sum = bin_sums[b] == 0.0 ? 0.0 : bin_sums[b] * gs;
-            bp->bins[a][r] = q != 0 ? sum / q : 0;
-            flat[b] = bp->bins[a][r];
+            rows[b] = q != 0 ? sum / q : 0;
         }
     }
+    const double* flat = rows;
     Blur_Vector_Group* bv = (Blur_Vector_Group*)calloc(1, sizeof(Blur_Vector_Group));
     bv->len_vectors = 10;
     bv->blur_vectors = (Blur_Vector*)calloc(10, sizeof(Blur_Vector));
-    vectorize_blur(flat.data(), na, nr, cfg.fft_streak_thresh, cfg.magnitude_thresh,
+    vectorize_blur(flat, na, nr, cfg.fft_streak_thresh, cfg.magnitude_thresh,
                    cfg.blur_cutoff_ratio_denom, bv->blur_vectors);
     Sharpnesses* sh = nullptr;
     if (crops) {   // get_variance_sharpness (src/filtering.c:151-183)
@@ -339,10 +341,18 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         return false;
     }
     const hipStream_t st = stream ? stream : c->stream;
+    while ((int)c->ev_img_fft.size() < n) {
+        hipEvent_t a, b;
+        PHD_HIP(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+        PHD_HIP(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+        c->ev_img_fft.push_back(a);
+        c->ev_img_dl.push_back(b);
+    }
     // a failed earlier call may have left work on the side streams
     PHD_HIP(hipStreamSynchronize(c->tail));
     PHD_HIP(hipStreamSynchronize(c->fft));
     PHD_HIP(hipStreamSynchronize(c->fft2));
+    PHD_HIP(hipStreamSynchronize(c->dl));
     const GridParams gp = make_grid(cfg);
     const GroupCenters gc = make_centers(gp);
     const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
@@ -434,6 +444,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                                          (double*)(dw + L.C(n, i) + L.c_sharp), sc));
             }
             PHD_HIP(hipEventRecord(c->ev_cols[b], sc));
+            PHD_HIP(hipEventRecord(c->ev_img_fft[i], sc));
         }
     }
     for (int g0 = 0; g0 < (pipe ? 0 : n); g0 += Q) {
@@ -461,6 +472,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                                          crop_arr.data() + 3 * ncrops, c->d_k255,
                                          (double*)(dw + L.C(n, i) + L.c_sharp), sf));
             }
+            PHD_HIP(hipEventRecord(c->ev_img_fft[i], sf));
         }
     }
     // the last column pass ends the FFT work (it waited for the last row pass)
@@ -564,16 +576,26 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipStreamWaitEvent(st, c->ev_tail, 0));
     PHD_HIP(hipStreamWaitEvent(st, c->ev_fft, 0));
     PHD_HIP(hipEventRecord(c->ev[3], st));
+    // image i's C record (bins, max partials, palette sums, sharpness) goes to
+    // the host once its column pass and the palette tail are done; the host
+    // assembles it while the later images' FFTs run
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
-    PHD_HIP(hipMemcpyAsync(hc, dw + L.C(n, 0), (size_t)n * L.c_bytes, hipMemcpyDeviceToHost, st));
-    PHD_HIP(hipEventRecord(c->ev[4], st));
+    const hipStream_t sd = c->dl;
+    PHD_HIP(hipStreamWaitEvent(sd, c->ev_tail, 0));
+    for (int i = 0; i < n; i++) {
+        PHD_HIP(hipStreamWaitEvent(sd, c->ev_img_fft[i], 0));
+        PHD_HIP(hipMemcpyAsync(hc + (size_t)i * L.c_bytes, dw + L.C(n, i), L.c_bytes, hipMemcpyDeviceToHost, sd));
+        PHD_HIP(hipEventRecord(c->ev_img_dl[i], sd));
+    }
+    PHD_HIP(hipEventRecord(c->ev[4], sd));
+    PHD_HIP(hipStreamWaitEvent(st, c->ev[4], 0));
     const auto t_dec = std::chrono::steady_clock::now();
-    PHD_HIP(hipEventSynchronize(c->ev[4]));
-    const auto t_sync = std::chrono::steady_clock::now();
-    c->prof.collect();
+    auto t_sync = t_dec;
 
     int failures = 0;
     for (int i = 0; i < n; i++) {
+        PHD_HIP(hipEventSynchronize(c->ev_img_dl[i]));
+        if (i == n - 1) t_sync = std::chrono::steady_clock::now();
         if (!ok[i]) {
             failures++;
             continue;
@@ -606,6 +628,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         }
     }
     const auto t_end = std::chrono::steady_clock::now();
+    PHD_HIP(hipEventSynchronize(c->ev[4]));
+    c->prof.collect();
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
@@ -808,7 +832,8 @@ extern "C" void free_full_report(Full_Report_Data** report) {
         free(r->color_palette);
     }
     if (r->blur_profile) {
-        for (int a = 0; a < r->blur_profile->num_angle_bins; a++) free(r->blur_profile->bins[a]);
+        // one block holds every row (assemble); a profile without angle bins has none
+        if (r->blur_profile->bins && r->blur_profile->num_angle_bins > 0) free(r->blur_profile->bins[0]);
         free(r->blur_profile->bins);
         free(r->blur_profile);
     }
