@@ -319,6 +319,28 @@ def test_hsv_group_exhaustive_rgb_cube(cfg):
     np.testing.assert_array_equal(d_gid.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("cfg", [{"coverage_thresh": 1.0}, {},
+                                 {"h_partitions": 36, "s_partitions": 4, "v_partitions": 5, "coverage_thresh": 1.0},
+                                 {"h_partitions": 15, "s_partitions": 3, "v_partitions": 2}])
+def test_table_k1_exhaustive_rgb_cube_palette(cfg):
+    """The production K1 (k1.hip: table classification, packed counts, one-pass
+    palette sums) over every RGB8 triple once: a 4096 x 4096 image holding the
+    whole 256^3 cube, full report against the oracle.  With coverage 1.0 every
+    non-empty group is a palette slot kept whole, so each group's count and
+    h / s / v sums over all its colours are compared directly."""
+    phd, L, _ = _phd()
+    from oracle import oracle as orc
+    k = np.arange(1 << 24, dtype=np.uint32)
+    cube = np.stack([(k >> 16) & 255, (k >> 8) & 255, k & 255], axis=1).astype(np.uint8).reshape(4096, 4096, 3)
+    rep = phd.get_report(cube, **cfg)
+    o = orc.palette(cube, **cfg)
+    cp = rep.color_palette
+    np.testing.assert_array_equal(np.array(cp.group_ids), o["valid_parents"])
+    np.testing.assert_array_equal(np.array(cp.quantities), o["palette_pct"])
+    np.testing.assert_allclose(np.array(cp.hsv).reshape(-1, 3), o["palette_hsv"], rtol=TIGHT_RTOL, atol=1e-12)
+    np.testing.assert_allclose(rep.average_saturation, o["average_saturation"], rtol=TIGHT_RTOL)
+
+
 FUSED_CFGS = [{}, {"h_partitions": 9}, {"h_partitions": 15, "s_partitions": 3, "v_partitions": 2},
               {"h_partitions": 5, "linked_list_size": 50}, {"h_partitions": 1, "s_partitions": 3},
               {"h_partitions": 72, "s_partitions": 2, "v_partitions": 2, "linked_list_size": 64},

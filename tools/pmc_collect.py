@@ -18,7 +18,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHORT = {"k_hsv_stats": "hsv_stats", "k_fft_rows": "fft_rows", "k_fft_cols": "fft_cols",
+SHORT = {"k_k1t": "hsv_stats", "k_rgb_stats": "rgb_stats", "k_hsv_stats": "hsv_stats", "k_fft_rows": "fft_rows", "k_fft_cols": "fft_cols",
          "k_rows_ct": "fft_rows", "k_cols_ct": "fft_cols", "k_cutoffs_b": "palette_cutoffs",
          "k_palette_sums_b": "palette_sums",
          "k_cutoffs": "palette_cutoffs", "k_palette_sums": "palette_sums", "k_sharp_pass": "sharpness"}

@@ -1,0 +1,7 @@
+set -e
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python tools/pmc_collect.py --tag r01 -- --steps 3 --warmup 1 --no-config3 > gpurun_out/pmc_collect.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline --steps 10 > gpurun_out/bench_prof.log 2>&1
+timeout -k 10 300 python bench.py > gpurun_out/bench_full.log 2>&1
+tail -1 gpurun_out/bench_full.log
