@@ -235,7 +235,7 @@ def main():
         line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
     if not args.no_config3 and world == 1:
         line["config3"] = config3(lib, last_error)
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(H, W, args.cpu_images)
     print(json.dumps(line), flush=True)
     if world > 1:
