@@ -58,9 +58,9 @@ __device__ __forceinline__ unsigned as1(u16x2 x) { return __builtin_bit_cast(uns
 // reciprocals, the code tables) lies below 64 KiB, so it is a DS
 // instruction's immediate offset (no address add per access); the per-run
 // records and the queue follow the 64 KiB code table.
-constexpr int kQueue = 2048;                              // deferred-pixel queue (chunk offsets, u16)
+constexpr int kQueue = 2048;                              // deferred-pixel queue (chunk offsets, u32)
 struct TVar {
-    int cells, gs2, ce, inv, red, code, rcell, cg, seg, r255, rmx, dq, qcnt, end;
+    int cells, gs2, ce, inv, k255, red, code, rcell, cg, seg, r255, rmx, dq, qcnt, end;
 };
 __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     const int C = 1 << cshift;
@@ -69,15 +69,16 @@ __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     v.gs2 = v.cells + 8 * (ncell + 1) * C;                          // (tl+1) * C * {h, s} f64
     v.ce = v.gs2 + 16 * (tl + 1) * C;                               // 256 u32
     v.inv = v.ce + 1024;                                            // 256 f64
-    v.red = v.inv + 2048;                                           // 16 waves x 8 x u64
+    v.k255 = v.inv + 2048;                                          // 256 f64: k / 255.0 (the exact path)
+    v.red = v.k255 + 2048;                                          // 16 waves x 8 x u64
     v.code = v.red + 1024;                                          // 65536 u8
     v.rcell = v.code + 65536;                                       // ncell u32
     v.cg = v.rcell + 4 * ncell;                                     // tl u32
     v.seg = v.cg + 4 * tl;                                          // tl u32
     v.r255 = v.seg + 4 * tl;                                        // tl u32
     v.rmx = (v.r255 + 4 * tl + 7) & ~7;                             // tl u64
-    v.dq = v.rmx + 8 * tl;                                          // kQueue u16
-    v.qcnt = v.dq + 2 * kQueue;                                     // u32 (+ pad)
+    v.dq = v.rmx + 8 * tl;                                          // kQueue u32
+    v.qcnt = v.dq + 4 * kQueue;                                     // u32 (+ pad)
     v.end = v.qcnt + 16;
     return v;
 }
@@ -163,7 +164,8 @@ __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k2
     const int num = isr ? kg - kb : (isg ? kb - kr : kr - kg);
     const int t = isr ? (num < 0 ? 3 : 0) : (isg ? 1 : 2);
     const int kd1 = max(kd, 1);
-    const int c = (240 * t * kd1 + 120 * num) / (X.lh * kd1);            // exact: on the boundary
+    const int n2 = 240 * t * kd1 + 120 * num, D = X.lh * kd1;
+    const int c = (int)(((float)n2 + 0.5f) * __builtin_amdgcn_rcpf((float)D));   // as t_pixel: exact
     const double B = (double)c * (double)X.lh * 0.5;
     const int ch = c - X.hp;
     int below;
@@ -278,13 +280,17 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
     unsigned* seg = reinterpret_cast<unsigned*>(smem + V.seg);
     unsigned* r255 = reinterpret_cast<unsigned*>(smem + V.r255);
     unsigned long long* rmx = reinterpret_cast<unsigned long long*>(smem + V.rmx);
-    unsigned short* dq = reinterpret_cast<unsigned short*>(smem + V.dq);
+    unsigned* dq = reinterpret_cast<unsigned*>(smem + V.dq);
+    double* k255 = reinterpret_cast<double*>(smem + V.k255);
     unsigned* qcnt = reinterpret_cast<unsigned*>(smem + V.qcnt);
     {
         const uint4* src = reinterpret_cast<const uint4*>(tabs->code8);
         uint4* dst = reinterpret_cast<uint4*>(code8);
         for (int i = tid; i < 65536 / 16; i += kT) dst[i] = src[i];
-        for (int i = tid; i < 256; i += kT) inv[i] = tabs->inv[i];
+        for (int i = tid; i < 256; i += kT) {
+            inv[i] = tabs->inv[i];
+            k255[i] = k255g[i];
+        }
         unsigned* z = reinterpret_cast<unsigned*>(smem);
         for (int i = tid; i < V.ce / 4; i += kT) z[i] = 0u;                        // cells, h/s sums
         for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;         // run records, queue
@@ -354,7 +360,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
                 m.qr += kr * kr; m.qg += kg * kg; m.qb += kb * kb;
                 const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
                 if (t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, t_read(kmx, kmx - kmn, code8, inv), cells, gs2, X, 0))
-                    t_exact(kr, kg, kb, k255g, gp, code8, inv, cells, gs2, X);
+                    t_exact(kr, kg, kb, k255, gp, code8, inv, cells, gs2, X);
             }
         }
         // deferred pixels: queued in LDS (chunk offsets) and resolved by all
@@ -367,10 +373,10 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
                 emask &= emask - 1;
                 const int off = 4 * tid + 4 * kT * (bt >> 2) + (bt & 3);
                 if (pos < kQueue) {
-                    dq[pos++] = (unsigned short)off;
+                    dq[pos++] = (unsigned)off;
                 } else {
                     const long p = base + off;
-                    t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255g, gp, code8, inv, cells, gs2, X);
+                    t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp, code8, inv, cells, gs2, X);
                 }
             }
         }
@@ -381,7 +387,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
         if (nq > 0) {
             for (int i = tid; i < nq; i += kT) {
                 const long p = base + dq[i];
-                t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255g, gp, code8, inv, cells, gs2, X);
+                t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp, code8, inv, cells, gs2, X);
             }
             __syncthreads();
         }
