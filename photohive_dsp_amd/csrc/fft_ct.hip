@@ -81,7 +81,8 @@ template <int W, int T, int... Rs>
 __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* __restrict__ img, int H,
                                                const unsigned long long* __restrict__ sums,
                                                const double* __restrict__ k255g, const double2* __restrict__ twg,
-                                               double2* __restrict__ inter, int ablate_arg) {
+                                               double2* __restrict__ inter, int ablate_arg,
+                                               unsigned long long* __restrict__ rsum) {
     using K = RowK<W, T, Rs...>;
     const int ablate = PHD_ABL(ablate_arg);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -115,6 +116,7 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
     int s = 0, pr = pair_of(0);
     if (pr < P) fetch(pr);
     __syncthreads();
+    unsigned cs[3] = {0u, 0u, 0u};    // this thread's channel sums (u32: a few row pairs of bytes)
     const int rot = (tid >> 1) & 3;   // b128 write swizzle: 8 lanes of a group hit 8 distinct 16-B slots
     // one row pair.  The loop head is reached with the same memory operations in
     // flight on every path (the prefetch, then the stores: a step's or, before
@@ -145,6 +147,11 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
                     const double p1 = kWr * byte_of(rg[j][1], 3 * e) + kWg * byte_of(rg[j][1], 3 * e + 1) +
                                       kWb * byte_of(rg[j][1], 3 * e + 2);
                     z[e] = make_double2(p0, two ? p1 : 0.0);
+                    // the channel sums of get_rgb_statistics' means (the column pass's
+                    // DC bias), exact integers: the FFTs need nothing from K1
+                    cs[0] += byte_of(rg[j][0], 3 * e) + (two ? byte_of(rg[j][1], 3 * e) : 0);
+                    cs[1] += byte_of(rg[j][0], 3 * e + 1) + (two ? byte_of(rg[j][1], 3 * e + 1) : 0);
+                    cs[2] += byte_of(rg[j][0], 3 * e + 2) + (two ? byte_of(rg[j][1], 3 * e + 2) : 0);
                 }
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
@@ -188,6 +195,22 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
         pr = prn;
     };
     while (pr < P) step();
+    if (rsum) {
+        // block sums through LDS (free after the last step's barrier), one atomic per channel
+        unsigned long long* red = reinterpret_cast<unsigned long long*>(smem);
+        unsigned long long w3[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) w3[c] = wave_sum((unsigned long long)cs[c]);
+        if (lane_id() == 0)
+#pragma unroll
+            for (int c = 0; c < 3; c++) red[(tid >> 6) * 3 + c] = w3[c];
+        __syncthreads();
+        if (tid < 3) {
+            unsigned long long t = 0;
+            for (int w = 0; w < T / 64; w++) t += red[w * 3 + tid];
+            if (t) atomicAdd(&rsum[tid], t);
+        }
+    }
 }
 
 // log(p) for p >= 1: e ln2 + log(m) with m = frexp mantissa and log(m) in fp32
@@ -409,14 +432,14 @@ int resident_grid(K kernel, int threads, size_t lds) {
 
 template <int W, int T, int... Rs>
 hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, const double* k255,
-                   const double2* tw, double2* inter, hipStream_t st) {
+                   const double2* tw, double2* inter, unsigned long long* rsum, hipStream_t st) {
     const size_t lds = RowK<W, T, Rs...>::lds;
     static const int grid = [&] {
         const int g = resident_grid(k_rows_ct<W, T, Rs...>, T, lds) / 32 * 32;   // schedule needs % 32
         return g > 32 ? g : 32;
     }();
     hipLaunchKernelGGL((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
-                       g_ablate);
+                       g_ablate, rsum);
     return hipGetLastError();
 }
 
@@ -506,10 +529,11 @@ int fft_cols_ct_blocks(int height, int wf, int nbins) {
 }
 
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
-                              const double* k255, const double2* tw, double2* inter, hipStream_t st) {
+                              const double* k255, const double2* tw, double2* inter, hipStream_t st,
+                              unsigned long long* rsum) {
     const int n_ = width;
 #define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, st);
+    if (n_ == N && V == v_) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, rsum, st);
     PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
 #undef PHD_X
     return hipErrorInvalidValue;

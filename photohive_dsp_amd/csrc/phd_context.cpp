@@ -227,8 +227,9 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
 }
 
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
-                           const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st) {
-    return s.ct ? launch_fft_rows_ct(img, height, width, sums, k255, s.tw_r, inter, st)
+                           const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st,
+                           unsigned long long* rsum) {
+    return s.ct ? launch_fft_rows_ct(img, height, width, sums, k255, s.tw_r, inter, st, rsum)
                 : launch_fft_rows(img, height, width, s.prow->plan, sums, k255, inter, st);
 }
 

@@ -151,7 +151,8 @@ struct FftSel {
 };
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s);
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
-                           const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st);
+                           const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st,
+                           unsigned long long* rsum = nullptr);
 // sums: K1's channel sums of the image (the compile-time column pass removes the DC bias)
 hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int width, int wf,
                            const uint16_t* binmap, int nbins, double* bin_sums, double* fmax_part,

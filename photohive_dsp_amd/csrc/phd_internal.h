@@ -221,7 +221,8 @@ int fft_cols_ct_blocks(int height, int wf, int nbins);
 // tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built).
 // The row pass transforms the luma as is (sums unused): it does not wait for K1.
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
-                              const double* k255, const double2* tw, double2* inter, hipStream_t st);
+                              const double* k255, const double2* tw, double2* inter, hipStream_t st,
+                              unsigned long long* rsum = nullptr);
 // The column pass removes the DC bias (K1's channel sums) from column 0 first.
 // dbg (optional): the power spectrum, column-major [wf][height]
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,

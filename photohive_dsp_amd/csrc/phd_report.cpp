@@ -31,7 +31,7 @@ size_t al(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 struct Layout {
     // per-image records
     size_t a_sums, a_hist, a_spart, a_gsum, a_gcell, a_bytes;  // read back after K1 (zeroed)
-    size_t c_bins, c_fmax, c_pal, c_sharp, c_bytes;         // read back at the end (zeroed)
+    size_t c_bins, c_fmax, c_pal, c_sharp, c_rsum, c_bytes; // read back at the end (zeroed)
     size_t b_rules, b_search, b_off, b_bytes;               // uploaded before K3
     size_t chunk_bytes;                                      // device only
     size_t ptr_bytes;                                        // image pointer array (pinned -> device)
@@ -61,7 +61,8 @@ Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolbl
     L.c_fmax = al(sizeof(double) * nbins);
     L.c_pal = L.c_fmax + al(sizeof(double) * (ncolblocks > 0 ? ncolblocks : 1));
     L.c_sharp = L.c_pal + al(sizeof(double) * 4 * tl);
-    L.c_bytes = L.c_sharp + al(sizeof(double) * 2 * (ncrops > 0 ? ncrops : 1));
+    L.c_rsum = L.c_sharp + al(sizeof(double) * 2 * (ncrops > 0 ? ncrops : 1));
+    L.c_bytes = L.c_rsum + al(3 * sizeof(unsigned long long));
     L.b_rules = 0;
     L.b_search = al(sizeof(GroupRule) * tl);
     L.b_off = L.b_search + al(sizeof(int) * tl);
@@ -415,20 +416,28 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // since K1's persistent blocks leave no room for them, and it blurs the
     // per-kernel event timings, so by default the FFTs follow K1)
     const hipStream_t sf = c->fft;
+    // PHD_FFT_OVERLAP=1 (compile-time plans): the row pass sums the channels
+    // itself (the column pass's DC bias), so the FFT chain needs nothing from
+    // K1 and runs beside it.  Measured slower (5.75k vs 6.05k images/s: row
+    // passes sharing CUs with K1 take 92 us instead of 49), so by default the
+    // FFTs follow K1 and take its channel sums.
     static const bool overlap = getenv("PHD_FFT_OVERLAP") != nullptr;
+    const bool own_dc = fs.ct && overlap;
     PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
-    if (!fs.ct || !overlap) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+    if (!own_dc) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
     const size_t inter_elems = inter_one / sizeof(double2);
     const hipStream_t sc = c->fft2;
     if (pipe) {
-        PHD_HIP(hipStreamWaitEvent(sc, c->ev_k1, 0));            // DC removal needs K1's sums
+        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sc, c->ev_k1, 0));   // DC removal needs K1's sums
+        PHD_HIP(hipStreamWaitEvent(sc, c->ev_ws, 0));
         for (int i = 0; i < n; i++) {
             const int b = i & 1;
             double2* inter = c->d_inter + (size_t)b * inter_elems;
-            const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+            unsigned long long* rsum = own_dc ? (unsigned long long*)(dw + L.C(n, i) + L.c_rsum) : nullptr;
+            const unsigned long long* sums = own_dc ? rsum : (const unsigned long long*)(dw + L.A(i) + L.a_sums);
             if (i >= 2) PHD_HIP(hipStreamWaitEvent(sf, c->ev_cols[b], 0));   // image i-2's columns are done
             int ps = c->prof.begin(kFftRows, sf);
-            PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255, inter, sf));
+            PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255, inter, sf, rsum));
             c->prof.end(ps, sf);
             PHD_HIP(hipEventRecord(c->ev_rows[b], sf));
             PHD_HIP(hipStreamWaitEvent(sc, c->ev_rows[b], 0));
@@ -451,14 +460,16 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         const int g1 = std::min(n, g0 + Q);
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+            unsigned long long* rsum = own_dc ? (unsigned long long*)(dw + L.C(n, i) + L.c_rsum) : nullptr;
             const int ps = c->prof.begin(kFftRows, sf);
             PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255,
-                                    c->d_inter + (size_t)(i - g0) * inter_elems, sf));
+                                    c->d_inter + (size_t)(i - g0) * inter_elems, sf, rsum));
             c->prof.end(ps, sf);
         }
-        if (g0 == 0 && fs.ct) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+        if (g0 == 0 && fs.ct && !own_dc) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
         for (int i = g0; i < g1; i++) {
-            const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+            const unsigned long long* sums = own_dc ? (const unsigned long long*)(dw + L.C(n, i) + L.c_rsum)
+                                                    : (const unsigned long long*)(dw + L.A(i) + L.a_sums);
             double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
             double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
             const int ps = c->prof.begin(kFftCols, sf);
