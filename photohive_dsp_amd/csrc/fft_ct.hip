@@ -149,9 +149,11 @@ __global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* 
                     z[e] = make_double2(p0, two ? p1 : 0.0);
                     // the channel sums of get_rgb_statistics' means (the column pass's
                     // DC bias), exact integers: the FFTs need nothing from K1
-                    cs[0] += byte_of(rg[j][0], 3 * e) + (two ? byte_of(rg[j][1], 3 * e) : 0);
-                    cs[1] += byte_of(rg[j][0], 3 * e + 1) + (two ? byte_of(rg[j][1], 3 * e + 1) : 0);
-                    cs[2] += byte_of(rg[j][0], 3 * e + 2) + (two ? byte_of(rg[j][1], 3 * e + 2) : 0);
+                    if (rsum) {                                   // uniform
+                        cs[0] += byte_of(rg[j][0], 3 * e) + (two ? byte_of(rg[j][1], 3 * e) : 0);
+                        cs[1] += byte_of(rg[j][0], 3 * e + 1) + (two ? byte_of(rg[j][1], 3 * e + 1) : 0);
+                        cs[2] += byte_of(rg[j][0], 3 * e + 2) + (two ? byte_of(rg[j][1], 3 * e + 2) : 0);
+                    }
                 }
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
