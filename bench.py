@@ -39,7 +39,7 @@ def parse(argv=None):
     p.add_argument("--no-kernel-events", action="store_true",
                    help="do not bracket kernels with HIP events (roofline then null)")
     p.add_argument("--no-config3", action="store_true",
-                   help="skip the BASELINE config-3 line (512 x 1080p rgb2hsv + rgb_statistics pass)")
+                   help="skip the BASELINE config-3/4 objects (512 x 1080p statistics pass; FFT + blur path)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                    help="per-kernel PMC traffic summary written by tools/pmc_collect.py")
     return p.parse_args(argv)
@@ -99,6 +99,56 @@ def config3(lib, last_error, n=512, h=1080, w=1920, iters=10):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ab / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us, 2)}}
+
+
+def config4(lib, last_error, n=32, h=3000, w=4000, iters=3):
+    """BASELINE config 4 on one GPU: the FFT + blur-profile path alone
+    (phd_blur_batch_device) over n device-resident 4000x3000 images.  The
+    column pass is this path's dominant kernel: its algorithmic bytes are the
+    half spectrum read plus the bin map, 18 * H * (W/2+1) per image (SURVEY.md 8d
+    counts 3N + 32 H Wf = 228 MB for the whole path)."""
+    import numpy as np
+    import torch
+    from photohive_dsp_amd.core import make_config
+    from photohive_dsp_amd.structures import Blur_Vector
+    nb = h * w * 3
+    t = torch.empty(n * nb, dtype=torch.uint8, device="cuda")
+    for i in range(n):
+        assert lib.phd_fill_uniform_device(t[i * nb:].data_ptr(), nb, 1000 + i, None) == 0, last_error()
+    cfg = make_config()
+    bins = np.zeros((n, cfg.angle_partitions, cfg.radius_partitions))
+    vecs = (Blur_Vector * (10 * n))()
+    P = ctypes.POINTER(ctypes.c_double)
+
+    def run():
+        if lib.phd_blur_batch_device(t.data_ptr(), n, h, w, 0, ctypes.byref(cfg), bins.ctypes.data_as(P), vecs,
+                                     None) != 0:
+            raise RuntimeError(f"blur batch failed: {last_error()}")
+    run()
+    lib.phd_profile_kernels(0)
+    lib.phd_profile_kernels(0b110)                  # rows and columns
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        run()
+    wall = (time.perf_counter() - t0) / iters
+    us = {}
+    for k, name in ((1, "fft_rows"), (2, "fft_cols")):
+        tot, cnt = ctypes.c_double(), ctypes.c_long()
+        lib.phd_profile_read(k, ctypes.byref(tot), ctypes.byref(cnt))
+        us[name] = 1000 * tot.value / max(cnt.value, 1)
+    lib.phd_profile_kernels(0)
+    del t
+    torch.cuda.empty_cache()
+    wf = w // 2 + 1
+    ab = 18.0 * h * wf
+    return {"workload": f"{n} x {h}x{w} RGB8, FFT + blur_profile only, device-resident",
+            "images_per_s": round(n / wall, 1), "ms_per_batch_wall": round(1000 * wall, 3),
+            "kernel_us_per_image": {k: round(v, 2) for k, v in us.items()},
+            "roofline": {"kernel": "fft_cols", "bound": "hbm", "achieved": round(ab / (us["fft_cols"] * 1e-6) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ab / (us["fft_cols"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us["fft_cols"], 2)}}
 
 
 def algorithmic_bytes(kernel, h, w):
@@ -235,6 +285,7 @@ def main():
         line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
     if not args.no_config3 and world == 1:
         line["config3"] = config3(lib, last_error)
+        line["config4"] = config4(lib, last_error)
     if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(H, W, args.cpu_images)
     print(json.dumps(line), flush=True)

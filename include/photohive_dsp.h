@@ -153,6 +153,18 @@ int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, int height, i
                                size_t image_stride, RGB_Statistics* stats, double* avg_saturation,
                                void* stream);
 
+/* The FFT + blur-profile path alone over n device-resident RGB8 images of one
+ * size (BASELINE.json config 4): rgb2pgm, remove_dc_bias, pgm_fft,
+ * pgm_normalize_fft, cartesian_to_polar_conversion, calculate_blur_profile
+ * and vectorize_blur_profile (src/image_processing.c:505-512,
+ * src/blur_profile.c:34-126,233-238,324-458, src/fft_processing.c:18-63,
+ * 173-213) as get_full_report_data runs them (src/interface.c:50,62-86).
+ * bins_out: n x angle_partitions x radius_partitions doubles (the
+ * Blur_Profile bins, angle-major); vectors_out: n x 10 Blur_Vector.  The
+ * values equal the full report's.  0 or -1. */
+int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int height, int width, size_t image_stride,
+                          const phd_config* cfg, double* bins_out, Blur_Vector* vectors_out, void* stream);
+
 /* A batch of host images of any sizes (config 5 of BASELINE.json). */
 int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
                         int n_images, const phd_config* cfg, Full_Report_Data** out, int* status);

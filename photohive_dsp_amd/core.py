@@ -230,6 +230,26 @@ def hsv_stats_device(images, stream=None):
     return list(stats), list(sat)
 
 
+def blur_profiles_device(images, stream=None, **kw):
+    """The FFT + blur-profile path alone (BASELINE config 4; rgb2pgm, pgm_fft,
+    calculate_blur_profile, vectorize_blur_profile) for a uint8 torch tensor
+    [N, H, W, 3] on the current GPU: returns (bins [N, angle, radius] float64,
+    [[(angle, magnitude)] * 10] * N) -- the full report's values."""
+    from .structures import Blur_Vector
+    if images.dtype.itemsize != 1 or images.dim() != 4 or images.shape[3] != 3 or not images.is_contiguous():
+        raise ValueError("expected a contiguous uint8 [N, H, W, 3] device tensor")
+    n, h, w = int(images.shape[0]), int(images.shape[1]), int(images.shape[2])
+    cfg = make_config(**kw)
+    na, nr = cfg.angle_partitions, cfg.radius_partitions
+    bins = np.zeros((n, na, nr), dtype=np.float64)
+    vecs = (Blur_Vector * (10 * n))()
+    s = stream.cuda_stream if stream is not None else None
+    if lib.phd_blur_batch_device(images.data_ptr(), n, h, w, 0, ctypes.byref(cfg),
+                                 bins.ctypes.data_as(POINTER(ctypes.c_double)), vecs, s) != 0:
+        raise RuntimeError(f"blur_profiles_device failed: {last_error()}")
+    return bins, [[(vecs[10 * i + k].angle, vecs[10 * i + k].magnitude) for k in range(10)] for i in range(n)]
+
+
 def set_bounding_boxes(bounding_boxes):
     """core.py:489-515."""
     n = len(bounding_boxes)

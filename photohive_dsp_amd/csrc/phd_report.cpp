@@ -126,6 +126,21 @@ float ms_between(hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
+// pgm_normalize_fft's G_s (src/fft_processing.c:192) applied to the binned
+// sums of log(p); calculate_blur_profile's averaging (src/blur_profile.c:106-116);
+// vectorize_blur_profile (src/blur_profile.c:324-416).  flat: na x nr.
+void finish_blur(const BlurTable& tbl, const double* bin_sums, double fmax, const phd_config& cfg, double* flat,
+                 Blur_Vector* vectors) {
+    const int na = cfg.angle_partitions, nr = cfg.radius_partitions;
+    const double gs = 1 / (2 * std::log(std::sqrt(fmax) + 1));
+    for (size_t b = 0; b < (size_t)na * nr; b++) {
+        const double q = (double)tbl.counts[b];
+        const double sum = bin_sums[b] == 0.0 ? 0.0 : bin_sums[b] * gs;
+        flat[b] = q != 0 ? sum / q : 0;
+    }
+    vectorize_blur(flat, na, nr, cfg.fft_streak_thresh, cfg.magnitude_thresh, cfg.blur_cutoff_ratio_denom, vectors);
+}
+
 Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const PaletteDecision& dec,
                            const double* pal, long n_hsv, const BlurTable& tbl, const double* bin_sums,
                            double fmax, const phd_config& cfg, const Crop_Boundaries* crops,
@@ -173,22 +188,11 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
     // block (free_full_report frees bins[0] and the pointer array)
     bp->bins = (Bin**)malloc(sizeof(Bin*) * na);
     Bin* rows = (Bin*)calloc((size_t)na * nr > 0 ? (size_t)na * nr : 1, sizeof(Bin));
-    const double gs = 1 / (2 * std::log(std::sqrt(fmax) + 1));
-    for (int a = 0; a < na; a++) {
-        bp->bins[a] = rows + (size_t)a * nr;
-        for (int r = 0; r < nr; r++) {
-            const size_t b = (size_t)a * nr + r;
-            const double q = (double)tbl.counts[b];
-            const double sum = bin_sums[b] == 0.0 ? 0.0 : bin_sums[b] * gs;
-            rows[b] = q != 0 ? sum / q : 0;
-        }
-    }
-    const double* flat = rows;
+    for (int a = 0; a < na; a++) bp->bins[a] = rows + (size_t)a * nr;
     Blur_Vector_Group* bv = (Blur_Vector_Group*)calloc(1, sizeof(Blur_Vector_Group));
     bv->len_vectors = 10;
     bv->blur_vectors = (Blur_Vector*)calloc(10, sizeof(Blur_Vector));
-    vectorize_blur(flat, na, nr, cfg.fft_streak_thresh, cfg.magnitude_thresh,
-                   cfg.blur_cutoff_ratio_denom, bv->blur_vectors);
+    finish_blur(tbl, bin_sums, fmax, cfg, rows, bv->blur_vectors);
     Sharpnesses* sh = nullptr;
     if (crops) {   // get_variance_sharpness (src/filtering.c:151-183)
         sh = (Sharpnesses*)malloc(sizeof(Sharpnesses));
@@ -937,6 +941,107 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
         double sacc = 0.0;
         for (int k = 0; k < nchunks; k++) sacc += sp[k];
         avg_saturation[i] = sacc / (double)npix;
+    }
+    return 0;
+}
+
+// The FFT + blur-profile path alone (BASELINE config 4): the row and column
+// passes per image, the channel sums of remove_dc_bias from the row pass
+// (compile-time plans) or the statistics pass (others), one read-back.
+extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
+                                     size_t image_stride, const phd_config* cfg, double* bins_out,
+                                     Blur_Vector* vectors_out, void* stream) {
+    clear_error();
+    if (!d_rgb || !cfg || !bins_out || !vectors_out || n_images <= 0) {
+        set_error("phd_blur_batch_device: bad arguments");
+        return -1;
+    }
+    std::string why;
+    if (!validate_config(*cfg, &why)) {
+        set_error(why);
+        return -1;
+    }
+    if (!precheck(height, width)) return -1;
+    if (width > kFftMaxLds || height > kFftMaxLds) {
+        set_error("image side above " + std::to_string(kFftMaxLds) + " px: the LDS-resident FFT rejects it");
+        return -1;
+    }
+    Context* c = get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
+    std::vector<const uint8_t*> imgs(n_images);
+    for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
+    const int nbins = cfg->radius_partitions * cfg->angle_partitions, wf = width / 2 + 1;
+    FftSel fs;
+    if (!select_fft(c, height, width, nbins, imgs.data(), n_images, &fs)) return -1;
+    const BlurTable* tbl = get_table(c, height, width, cfg->radius_partitions, cfg->angle_partitions);
+    if (!tbl) return -1;
+    // per image: bins, max partials, channel sums (+ the statistics pass's chunk slots)
+    const long npix = (long)height * width;
+    const int nchunks = (int)((npix + kChunk - 1) / kChunk);
+    const size_t r_bins = 0, r_fmax = al(sizeof(double) * nbins);
+    const size_t r_sums = r_fmax + al(sizeof(double) * (fs.col_blocks > 0 ? fs.col_blocks : 1));
+    const size_t r_spart = r_sums + al(6 * sizeof(unsigned long long));
+    const size_t rb = r_spart + al(sizeof(double) * nchunks);
+    const size_t ptrs = al(sizeof(void*) * (size_t)n_images);
+    const size_t inter_one = sizeof(double2) * ((size_t)(height + 1) * (wf + 1) + 1024);
+    if (!ensure_device(&c->d_ws, &c->ws_bytes, (size_t)n_images * rb + ptrs) ||
+        !ensure_pinned(c, (size_t)n_images * rb + ptrs) ||
+        !ensure_device((void**)&c->d_inter, &c->inter_bytes, inter_one))
+        return -1;
+    uint8_t* dw = (uint8_t*)c->d_ws;
+    uint8_t* hp = (uint8_t*)c->h_pin;
+    auto fail = [&](hipError_t e, const char* what) {
+        set_error(std::string("phd_blur_batch_device: ") + what + ": " + hipGetErrorString(e));
+        return -1;
+    };
+    hipError_t e;
+    if ((e = hipMemsetAsync(dw, 0, (size_t)n_images * rb, st)) != hipSuccess) return fail(e, "memset");
+    if (!fs.ct) {
+        // the runtime-plan row pass removes the DC bias itself: channel sums first
+        const uint8_t** hptr = (const uint8_t**)(hp + (size_t)n_images * rb);
+        for (int i = 0; i < n_images; i++) hptr[i] = imgs[i];
+        if ((e = hipMemcpyAsync(dw + (size_t)n_images * rb, hptr, sizeof(void*) * n_images, hipMemcpyHostToDevice,
+                                st)) != hipSuccess)
+            return fail(e, "pointer upload");
+        const GridParams gp = make_grid(*cfg);
+        const Context::Cls* cls = get_cls(c, gp);
+        if (!cls) return -1;
+        PaletteDev pd{};
+        pd.sums = (unsigned long long*)(dw + r_sums);
+        pd.s_part = (double*)(dw + r_spart);
+        if ((e = launch_hsv_stats_batch((const uint8_t* const*)(dw + (size_t)n_images * rb), n_images, height,
+                                        width, gp, cls->fc, cls->d, pd, (long)rb, 0, nchunks, c->d_k255, false,
+                                        false, all_aligned(hptr, n_images), st)) != hipSuccess)
+            return fail(e, "statistics pass");
+    }
+    for (int i = 0; i < n_images; i++) {
+        unsigned long long* sums = (unsigned long long*)(dw + (size_t)i * rb + r_sums);
+        int ps = c->prof.begin(kFftRows, st);
+        if ((e = launch_rows_sel(fs, imgs[i], height, width, sums, c->d_k255, c->d_inter, st,
+                                 fs.ct ? sums : nullptr)) != hipSuccess)
+            return fail(e, "row pass");
+        c->prof.end(ps, st);
+        ps = c->prof.begin(kFftCols, st);
+        if ((e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map, nbins,
+                                 (double*)(dw + (size_t)i * rb + r_bins), (double*)(dw + (size_t)i * rb + r_fmax),
+                                 sums, nullptr, st)) != hipSuccess)
+            return fail(e, "column pass");
+        c->prof.end(ps, st);
+    }
+    if ((e = hipMemcpyAsync(hp, dw, (size_t)n_images * rb, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return fail(e, "readback");
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return fail(e, "sync");
+    c->prof.collect();
+    for (int i = 0; i < n_images; i++) {
+        const uint8_t* r = hp + (size_t)i * rb;
+        const double* fpart = (const double*)(r + r_fmax);
+        double fmax = 0.0;
+        for (int b = 0; b < fs.col_blocks; b++) fmax = fpart[b] > fmax ? fpart[b] : fmax;
+        finish_blur(*tbl, (const double*)(r + r_bins), fmax, *cfg, bins_out + (size_t)i * nbins,
+                    vectors_out + (size_t)i * 10);
     }
     return 0;
 }

@@ -3,7 +3,7 @@ and argtypes as /root/reference/lib.py:20-37, plus the new entry points."""
 import ctypes
 import os
 
-from .structures import (Blur_Profile, Crop_Boundaries, Full_Report_Data, Image_PGM, Image_RGB,
+from .structures import (Blur_Profile, Blur_Vector, Crop_Boundaries, Full_Report_Data, Image_PGM, Image_RGB,
                          PhdConfig, RGB_Statistics)
 
 def _preload_torch_hip_runtime():
@@ -54,6 +54,10 @@ lib.phd_report_batch_device.restype = ctypes.c_int
 lib.phd_report_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_size_t, P(PhdConfig), P(P(Full_Report_Data)),
                                         P(ctypes.c_int), ctypes.c_void_p]
+lib.phd_blur_batch_device.restype = ctypes.c_int
+lib.phd_blur_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                      ctypes.POINTER(PhdConfig), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(Blur_Vector), ctypes.c_void_p]
 lib.phd_hsv_stats_batch_device.restype = ctypes.c_int
 lib.phd_hsv_stats_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_size_t, P(RGB_Statistics), P(ctypes.c_double),

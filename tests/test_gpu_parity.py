@@ -246,6 +246,25 @@ def test_hsv_stats_pass_batch_512_1080p_consistency():
     del t, v
 
 
+@pytest.mark.parametrize("kind,h,w", [("hblur", 3000, 4000), ("structured", 600, 800), ("motion", 401, 577)])
+def test_blur_batch_matches_full_report(kind, h, w):
+    """The FFT + blur-profile path alone (phd_blur_batch_device, config 4) gives
+    the full report's bins and vectors: the compile-time path takes the DC sums
+    from its own row pass, the runtime-plan path from the statistics pass, the
+    full report from K1 -- the same integers.  Bins agree to the last bits the
+    order of the column pass's fp64 atomics leaves free (1e-12)."""
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import blur_profiles_device, report_device
+    imgs = np.stack([synth.make(kind, h, w, 70 + i) for i in range(2)])
+    t = torch.from_numpy(imgs).cuda()
+    bins, vecs = blur_profiles_device(t)
+    reps = report_device(t)
+    for i, r in enumerate(reps):
+        np.testing.assert_allclose(bins[i], np.array(r.blur_profile.bins), rtol=1e-12, atol=1e-15)
+        assert vecs[i] == [(v.angle, v.magnitude) for v in r.blur_vectors]
+
+
 def test_mixed_size_host_batch():
     phd, L, _ = _phd()
     from photohive_dsp_amd import synth
