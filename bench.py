@@ -151,6 +151,49 @@ def config4(lib, last_error, n=32, h=3000, w=4000, iters=3):
                          "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us["fft_cols"], 2)}}
 
 
+def config5(lib, last_error, n=512, iters=2):
+    """BASELINE config 5 on one GPU: full reports of n device-resident images of
+    mixed sizes (shard.MIXED_SHAPES, 512^2 .. 6000x4000; 512 is one rank's share
+    of the 4096 at 8 GPUs) with h/s/v = 36/4/5, through
+    phd_report_batch_device_mixed (one batched run per size group)."""
+    import torch
+    from photohive_dsp_amd import shard
+    from photohive_dsp_amd.core import make_config
+    from photohive_dsp_amd.structures import Full_Report_Data
+    sizes = shard.mixed_sizes(n, 5)
+    ts = []
+    for i, (h, w) in enumerate(sizes):
+        t = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
+        assert lib.phd_fill_uniform_device(t.data_ptr(), t.numel(), 5000 + i, None) == 0, last_error()
+        ts.append(t)
+    cfg = make_config(h_partitions=36, s_partitions=4, v_partitions=5)
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+    hs = (ctypes.c_int * n)(*[h for h, _ in sizes])
+    ws = (ctypes.c_int * n)(*[w for _, w in sizes])
+    outs = (ctypes.POINTER(Full_Report_Data) * n)()
+    st = (ctypes.c_int * n)()
+
+    def run():
+        if lib.phd_report_batch_device_mixed(ptrs, hs, ws, n, ctypes.byref(cfg), outs, st, None) != 0:
+            raise RuntimeError(f"mixed batch failed: {last_error()}")
+        for i in range(n):
+            r = outs[i]
+            lib.free_full_report(ctypes.byref(r))
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        run()
+    wall = (time.perf_counter() - t0) / iters
+    mpx = sum(h * w for h, w in sizes) / 1e6
+    del ts
+    torch.cuda.empty_cache()
+    return {"workload": f"{n} mixed-size RGB8 images (seed 5, {len(set(sizes))} sizes, {mpx:.0f} Mpx), "
+                        "full report, h/s/v 36/4/5, device-resident",
+            "images_per_s": round(n / wall, 1), "megapixels_per_s": round(mpx / wall, 1),
+            "ms_per_batch_wall": round(1000 * wall, 2)}
+
+
 def algorithmic_bytes(kernel, h, w):
     """Bytes one launch must move: RGB8 reads of the pixel passes,
     the fp64-complex half spectrum written by the row pass and read by the column pass."""
@@ -286,6 +329,7 @@ def main():
     if not args.no_config3 and world == 1:
         line["config3"] = config3(lib, last_error)
         line["config4"] = config4(lib, last_error)
+        line["config5"] = config5(lib, last_error)
     if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(H, W, args.cpu_images)
     print(json.dumps(line), flush=True)

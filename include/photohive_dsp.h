@@ -165,6 +165,13 @@ int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, int height, i
 int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int height, int width, size_t image_stride,
                           const phd_config* cfg, double* bins_out, Blur_Vector* vectors_out, void* stream);
 
+/* Device-resident images of any sizes (config 5 of BASELINE.json): one
+ * batched run per group of same-size images.  Returns 0 when every image
+ * succeeded, else the number of failures, or -1 on a setup error. */
+int phd_report_batch_device_mixed(const uint8_t* const* d_images, const int* heights, const int* widths,
+                                  int n_images, const phd_config* cfg, Full_Report_Data** out, int* status,
+                                  void* stream);
+
 /* A batch of host images of any sizes (config 5 of BASELINE.json). */
 int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
                         int n_images, const phd_config* cfg, Full_Report_Data** out, int* status);

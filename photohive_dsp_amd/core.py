@@ -215,6 +215,28 @@ def report_device(images, stream=None, **kw):
     return res
 
 
+def reports_device_mixed(images, stream=None, **kw):
+    """Reports for a list of uint8 torch tensors [H, W, 3] of any sizes resident
+    on the current GPU (BASELINE config 5): one batched run per group of
+    same-size images (phd_report_batch_device_mixed)."""
+    for im in images:
+        if im.dtype.itemsize != 1 or im.dim() != 3 or im.shape[2] != 3 or not im.is_contiguous():
+            raise ValueError("expected contiguous uint8 [H, W, 3] device tensors")
+    n = len(images)
+    cfg = make_config(**kw)
+    ptrs = (ctypes.c_void_p * n)(*[im.data_ptr() for im in images])
+    hs = (ctypes.c_int * n)(*[int(im.shape[0]) for im in images])
+    ws = (ctypes.c_int * n)(*[int(im.shape[1]) for im in images])
+    outs = (POINTER(Full_Report_Data) * n)()
+    st = (ctypes.c_int * n)()
+    s = stream.cuda_stream if stream is not None else None
+    lib.phd_report_batch_device_mixed(ptrs, hs, ws, n, ctypes.byref(cfg), outs, st, s)
+    res = [(_finish(outs[i], hs[i], ws[i], kw) if st[i] == 0 else None) for i in range(n)]
+    if any(r is None for r in res):
+        raise RuntimeError(f"reports_device_mixed failed: {last_error()}")
+    return res
+
+
 def hsv_stats_device(images, stream=None):
     """rgb2hsv + get_hsv_average + get_rgb_statistics (src/image_processing.c:372-417, 533-553)
     for a uint8 torch tensor [N, H, W, 3] on the current GPU: returns

@@ -75,10 +75,14 @@ struct RowK {
     static constexpr size_t lds = sizeof(double2) * (W + NTW);
     static_assert(W % 4 == 0, "row plans need W % 4 == 0");
     static_assert(Radices<Rs...>::product == W, "plan");
+    // waves per SIMD the launch bounds ask for: 2 blocks per CU, fewer when
+    // the LDS holds fewer (W = 6000: one block, so twice the VGPRs)
+    static constexpr int BPC = (int)((160 * 1024) / lds) < 2 ? (int)((160 * 1024) / lds) : 2;
+    static constexpr int MINW = (T >= 512 ? 4 : 2) * BPC / 2 > 0 ? (T >= 512 ? 4 : 2) * BPC / 2 : 1;
 };
 
 template <int W, int T, int... Rs>
-__global__ __launch_bounds__(T, T >= 512 ? 4 : 2) void k_rows_ct(const uint8_t* __restrict__ img, int H,
+__global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const uint8_t* __restrict__ img, int H,
                                                const unsigned long long* __restrict__ sums,
                                                const double* __restrict__ k255g, const double2* __restrict__ twg,
                                                double2* __restrict__ inter, int ablate_arg,
@@ -240,6 +244,10 @@ struct ColK {
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
     static size_t lds(int nbins) { return sizeof(double2) * (NC * H + NTW) + (GB ? 0 : sizeof(double) * nbins); }
     static_assert(Radices<Rs...>::product == H, "plan");
+    // waves per SIMD of the launch bounds: one-column blocks are sized for two
+    // resident blocks per CU, one when the column and twiddles fill the LDS
+    static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
+    static constexpr int MINW = NC == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2 : 1;
     static_assert(NC == 1 || NC == 2, "columns per block");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
 };
@@ -250,7 +258,7 @@ struct ColK {
 // each line is fetched once into that XCD's L2 (the grid is a multiple of 32).
 // one-column blocks are sized for two resident blocks per CU
 template <int H, int T, int CPB, int... Rs>
-__global__ __launch_bounds__((CPB & 3) * T, (CPB & 3) == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) : 1) void k_cols_ct(const double2* __restrict__ inter, int wf,
+__global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter, int wf,
                                                      const uint16_t* __restrict__ binmap, int nbins,
                                                      double* __restrict__ bin_sums, double* __restrict__ fmax_part,
                                                      const double2* __restrict__ twg,

@@ -922,6 +922,142 @@ __global__ __launch_bounds__(kPartThreads) void k_partial_sums_b(
     }
 }
 
+// The same sums with one walk per image instead of one per (image, group):
+// block (image, split) classifies every pixel of the image's prefix up to the
+// largest cutoff once, and a pixel of one of the image's partial groups
+// (LDS group -> entry map) before that group's cutoff adds its terms to the
+// entry's LDS accumulators (rare: a few hundred pixels per group).  With many
+// partial groups whose cutoffs lie deep in the image (fine grids: 36/4/5 on
+// uniform images keeps ~1000 of ~16k pixels per group, cutoffs ~700k pixels
+// in) this reads and classifies the prefix once instead of once per group.
+constexpr int kPartImgMax = 64;                   // partial groups per image (else k_partial_sums_b)
+struct PartImgLds {
+    static constexpr int se = K1Lds::qn;          // first entry, entry count
+    static constexpr int acc = K1Lds::area;       // kPartImgMax x 4 doubles
+    static constexpr int off = acc + 32 * kPartImgMax;
+    static constexpr int cut = off + 8 * kPartImgMax;
+    static constexpr int grp = cut + 4 * kPartImgMax;
+    static constexpr int slot = grp + 4 * kPartImgMax;
+    static constexpr int gent = slot + 4 * kPartImgMax;   // tl shorts
+    static size_t bytes(int tl) { return (size_t)gent + 2 * (size_t)tl; }
+};
+
+template <bool kAligned, bool kThr>
+__global__ __launch_bounds__(kPartThreads) void k_partial_sums_img(
+        const uint8_t* const* __restrict__ imgs, long npix, GridParams gp, FastCls fc,
+        const ClassTables* __restrict__ tabs, const double* __restrict__ k255g, const int2* __restrict__ entries,
+        int n_entries, const unsigned short* __restrict__ chunk_hist0, long h_stride,
+        const GroupRule* __restrict__ rules0, const double* __restrict__ off0, long b_stride, double* out0,
+        long c_stride) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const double* k255 = reinterpret_cast<const double*>(smem + K1Lds::k255);
+    const ClsEnt* ent = reinterpret_cast<const ClsEnt*>(smem + K1Lds::ent);
+    int* se = reinterpret_cast<int*>(smem + PartImgLds::se);
+    double* acc = reinterpret_cast<double*>(smem + PartImgLds::acc);
+    double* eoff = reinterpret_cast<double*>(smem + PartImgLds::off);
+    unsigned* ecut = reinterpret_cast<unsigned*>(smem + PartImgLds::cut);
+    int* egrp = reinterpret_cast<int*>(smem + PartImgLds::grp);
+    int* eslot = reinterpret_cast<int*>(smem + PartImgLds::slot);
+    short* gent = reinterpret_cast<short*>(smem + PartImgLds::gent);
+    const signed char* si8 = tabs->si8;
+    const int tid = threadIdx.x, img = blockIdx.x, tl = gp.tl;
+    stage_tables(smem, k255g, tabs);
+    if (tid < 2) se[tid] = 0;
+    for (int g = tid; g < tl; g += kPartThreads) gent[g] = -1;
+    __syncthreads();
+    // this image's entries: a contiguous run of the image-major list
+    for (int k = tid; k < n_entries; k += kPartThreads) {
+        if (entries[k].x != img) continue;
+        if (k == 0 || entries[k - 1].x != img) se[0] = k;
+        atomicAdd(&se[1], 1);
+    }
+    __syncthreads();
+    const int e0 = se[0], ne = se[1];
+    if (ne == 0) return;                                     // block-uniform
+    const uint8_t* ip = imgs[img];
+    const GroupRule* rules =
+            reinterpret_cast<const GroupRule*>(reinterpret_cast<const char*>(rules0) + img * b_stride);
+    const double* offs = reinterpret_cast<const double*>(reinterpret_cast<const char*>(off0) + img * b_stride);
+    const unsigned short* chunk_hist =
+            reinterpret_cast<const unsigned short*>(reinterpret_cast<const char*>(chunk_hist0) + img * h_stride);
+    for (int e = tid; e < ne; e += kPartThreads) {
+        const int g = entries[e0 + e].y;
+        const GroupRule r = rules[g];
+        gent[g] = (short)e;
+        egrp[e] = g;
+        eslot[e] = r.slot;
+        eoff[e] = offs[r.slot];
+        ecut[e] = (r.partial && r.keep > 0) ? r.cutoff : 0u;
+    }
+    for (int i = tid; i < 4 * ne; i += kPartThreads) acc[i] = 0.0;
+    __syncthreads();
+    unsigned cmax = 0;
+    for (int e = 0; e < ne; e++) cmax = max(cmax, ecut[e]);
+    // calculate_avg_hsv's terms of one kept pixel into entry e
+    auto put = [&](int e, int kr, int kg, int kb, double sv) {
+        double tp = hue_exact(kr, kg, kb, k255) + eoff[e];
+        tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
+        atomicAdd(&acc[4 * e + 0], tp);
+        atomicAdd(&acc[4 * e + 1], sv);
+        atomicAdd(&acc[4 * e + 2], v_of(max(kr, max(kg, kb)), k255));
+        atomicAdd(&acc[4 * e + 3], 1.0);
+    };
+    auto add = [&](long p, int kr, int kg, int kb) {
+        double sv;
+        const int g = exact_group_t<kThr>(kr, kg, kb, ent, si8, k255, gp, fc, sv);
+        const int e = g >= 0 ? gent[g] : -1;
+        if (e >= 0 && p < (long)ecut[e]) put(e, kr, kg, kb, sv);
+    };
+    constexpr int kUnit = 16 * kPartThreads;
+    const long full_end = npix & ~3L;
+    const long umax = cmax > 0 ? (long)(cmax - 1) / kUnit : -1;
+    for (long u = blockIdx.y; u <= umax; u += gridDim.y) {
+        // block-uniform: skip a unit no entry needs (past its cutoff or none of its pixels in the chunk)
+        const long ub = u * kUnit, ch = ub / kChunk;
+        bool any = false;
+        for (int e = 0; e < ne; e++) any |= ub < (long)ecut[e] && chunk_hist[ch * tl + egrp[e]] != 0;
+        if (!any) continue;
+        const long end = std::min<long>(ub + kUnit, (long)cmax);
+        unsigned w[4][3];
+        bool okg[4];
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            const long p0 = ub + 4L * tid + 4L * kPartThreads * st;
+            okg[st] = p0 + 3 < full_end;
+            load_group<kAligned>(ip, p0, okg[st], w[st]);
+        }
+#pragma unroll
+        for (int st = 0; st < 4; st++) {
+            const long p0 = ub + 4L * tid + 4L * kPartThreads * st;
+            if (p0 >= end) continue;
+            if (okg[st]) {
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (p0 + i < end)
+                        add(p0 + i, px_byte(w[st], 3 * i), px_byte(w[st], 3 * i + 1), px_byte(w[st], 3 * i + 2));
+            } else {
+                for (long p = p0; p < p0 + 4 && p < end && p < npix; p++) add(p, ip[3 * p], ip[3 * p + 1], ip[3 * p + 2]);
+            }
+        }
+    }
+    if (blockIdx.y == 0)
+        for (int e = tid; e < ne; e += kPartThreads) {
+            const GroupRule r = rules[egrp[e]];
+            if (r.partial && r.dangle && r.last != 0xFFFFFFFFu && r.last >= ecut[e]) {
+                const long p = r.last;                       // the dangling node's pixel
+                const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
+                double sv;
+                if (exact_group_t<kThr>(kr, kg, kb, ent, si8, k255, gp, fc, sv) == egrp[e]) put(e, kr, kg, kb, sv);
+            }
+        }
+    __syncthreads();
+    double* out = reinterpret_cast<double*>(reinterpret_cast<char*>(out0) + img * c_stride);
+    for (int i = tid; i < 4 * ne; i += kPartThreads) {
+        const double a = acc[i];
+        if (a != 0.0) atomicAdd(&out[4 * eslot[i >> 2] + (i & 3)], a);
+    }
+}
+
 // K1 for downsample_rate > 1: HSV over the decimated pixels only (gathered).
 template <bool kThr>
 __global__ __launch_bounds__(kThreads) void k_hsv_ds(const uint8_t* __restrict__ img, long npix,
@@ -1448,11 +1584,28 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
                                      const ClassTables* tabs, const double* k255, const int2* entries,
                                      int n_entries, const unsigned short* chunk_hist0, long h_stride,
                                      const GroupRule* rules0, const double* off0, long b_stride, double* out0,
-                                     long c_stride, hipStream_t st) {
+                                     long c_stride, int max_per_image, hipStream_t st) {
     if (n_entries <= 0) return hipSuccess;
     const long npix = (long)height * width;
     bool aligned = true;
     for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
+    static const bool per_group = getenv("PHD_PARTIAL_PER_GROUP") != nullptr;
+    if (!per_group && max_per_image <= kPartImgMax && max_per_image > 1) {
+        const size_t lds = PartImgLds::bytes(gp.tl);
+        const dim3 grid(n, 64);
+#define PHD_PI_LAUNCH(A, T)                                                                                     \
+    hipLaunchKernelGGL((k_partial_sums_img<A, T>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc, tabs, \
+                       k255, entries, n_entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride)
+        if (fc.use_thr) {
+            if (aligned) PHD_PI_LAUNCH(true, true);
+            else PHD_PI_LAUNCH(false, true);
+        } else {
+            if (aligned) PHD_PI_LAUNCH(true, false);
+            else PHD_PI_LAUNCH(false, false);
+        }
+#undef PHD_PI_LAUNCH
+        return hipGetLastError();
+    }
     const size_t lds = K1Lds::qn;
     const dim3 grid(n_entries, 32);
     if (fc.use_thr) {

@@ -287,6 +287,8 @@ const Context::Cls* get_cls(Context* c, const GridParams& gp) {
     Context::Cls e;
     ClassTables t;
     make_class_tables(gp, &e.fc, &t);
+    e.gc = make_centers(gp);
+    e.near = make_near_order(gp, e.gc);
     if (hipMalloc(&e.d, sizeof(ClassTables)) != hipSuccess ||
         hipMemcpy(e.d, &t, sizeof(ClassTables), hipMemcpyHostToDevice) != hipSuccess) {
         set_error("classification table upload failed");

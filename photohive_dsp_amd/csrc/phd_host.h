@@ -48,9 +48,16 @@ struct PaletteDecision {
     std::vector<double> off;             // 180 - h_centre(parent)
     std::vector<int> search;             // groups needing the device cutoff search
 };
-// find_valid_octree_parents + group_irregular_pixels as keep rules.
+// For each group i, every group ordered by (node_distance(i, p), p): the
+// nearest-parent search of group_irregular_pixels walks it to the first
+// parent instead of measuring every parent.  tl * tl u16; empty above
+// kNearMaxGroups groups (then the search measures every parent).
+constexpr int kNearMaxGroups = 2048;
+std::vector<uint16_t> make_near_order(const GridParams& gp, const GroupCenters& gc);
+// find_valid_octree_parents + group_irregular_pixels as keep rules.  near:
+// make_near_order's table or nullptr.
 bool decide_palette(const GridParams& gp, const GroupCenters& gc, const unsigned* hist, long n_hsv,
-                    const phd_config& cfg, PaletteDecision* out);
+                    const phd_config& cfg, PaletteDecision* out, const uint16_t* near = nullptr);
 
 // ---- blur profile helpers (host) ------------------------------------------
 struct BlurTable {
@@ -97,6 +104,8 @@ struct Context {
     struct Cls {
         FastCls fc;
         ClassTables* d = nullptr;
+        GroupCenters gc;                            // initialize_octree's centres
+        std::vector<uint16_t> near;                 // make_near_order
     };
     std::map<std::tuple<int, int, int, double, double>, Cls> cls;
     // grow-only workspaces

@@ -137,12 +137,14 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
 bool fused_palette_ok(const GridParams& gp);
 // Fused palette: the slot sums of the partial (tie-overflow) groups, added
 // into out0 (every c_stride bytes) after Kcut filled their cutoff / last.
+// entries: (image, group), image-major; max_per_image: the most entries of
+// one image (one prefix walk per image when small, else one per entry).
 hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t* const* h_imgs, int n,
                                      int height, int width, const GridParams& gp, const FastCls& fc,
                                      const ClassTables* tabs, const double* k255, const int2* entries,
                                      int n_entries, const unsigned short* chunk_hist0, long h_stride,
                                      const GroupRule* rules0, const double* off0, long b_stride, double* out0,
-                                     long c_stride, hipStream_t st);
+                                     long c_stride, int max_per_image, hipStream_t st);
 // Kcut and K3 over a batch (ds == 1): entries = (image, group) pairs needing a
 // cutoff search; B records (rules at rules0, slot offsets at off0) every
 // b_stride bytes; palette sums at out0 every c_stride bytes.  h_imgs: the same
@@ -198,7 +200,10 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(4000, 1, 256, 25, 16, 10)     \
     X(4000, 2, 400, 25, 16, 10)     \
     X(4000, 3, 256, 5, 8, 10, 10)   \
-    X(4000, 4, 384, 5, 8, 10, 10)
+    X(4000, 4, 384, 5, 8, 10, 10)   \
+    X(6000, 0, 512, 6, 10, 10, 10)  \
+    X(3000, 0, 384, 5, 6, 10, 10)   \
+    X(2000, 0, 256, 5, 4, 10, 10)
 // columns: X(length, variant, threads per column, flags, radices...); flags:
 // columns per block (1, 2) | 4 no register prefetch | 8 bins by global atomics.
 // Measured at 4000x3000 (tools/ct_sweep.py): v0 54.8 us, v2 55.5, v3 56.0,
@@ -210,7 +215,10 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 2, 256, 5, 15, 20, 10)     \
     X(3000, 3, 256, 5, 25, 12, 10)     \
     X(3000, 4, 512, 5, 5, 6, 10, 10)   \
-    X(3000, 5, 300, 5, 5, 6, 10, 10)
+    X(3000, 5, 300, 5, 5, 6, 10, 10)   \
+    X(6000, 0, 512, 5, 15, 20, 20)     \
+    X(4000, 0, 256, 5, 10, 20, 20)     \
+    X(2000, 0, 256, 5, 10, 10, 20)
 int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);

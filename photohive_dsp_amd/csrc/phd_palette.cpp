@@ -15,6 +15,7 @@
 //    through the parent's stale tail pointer: the pixels that fit the tail node
 //    survive, and on overflow only the group's last pixel survives as a
 //    dangling node until the next event on that parent replaces it.
+#include <algorithm>
 #include <cmath>
 #include <climits>
 #include <cstring>
@@ -149,13 +150,6 @@ float saliency(unsigned q, double s, double v, float qw, float svw) {
     return sal * 1000;
 }
 
-// compare_quantities' (int)(sal_b - sal_a), as the x86 conversion behaves.
-int compare(float sal_a, float sal_b) {
-    const float d = sal_b - sal_a;
-    if (!(d > -2147483648.0f && d < 2147483648.0f)) return INT_MIN;
-    return (int)d;
-}
-
 double node_distance(const GridParams& g, const GroupCenters& c, int gi, int pi) {
     const int gray_start = g.tl - (g.ng + 1), black = g.tl - 1;
     if (gi < gray_start && pi < gray_start) {
@@ -174,21 +168,97 @@ double node_distance(const GridParams& g, const GroupCenters& c, int gi, int pi)
     return vd * vd;
 }
 
+// compare_quantities(x, y) < 0 for the element x being inserted and its left
+// neighbour y, i.e. (int)(y - x) < 0 as the x86 conversion behaves (INT_MIN
+// for |d| >= 2^31 or NaN): the insertion sort moves x past y.
+inline bool moves_past(float y, float x) {
+    const float d = y - x;
+    return !(d > -1.0f && d < 2147483648.0f);
+}
+
 }  // namespace
 
+std::vector<uint16_t> make_near_order(const GridParams& g, const GroupCenters& gc) {
+    const int tl = g.tl;
+    std::vector<uint16_t> near;
+    if (tl > kNearMaxGroups) return near;
+    near.resize((size_t)tl * tl);
+    std::vector<double> d(tl);
+    for (int i = 0; i < tl; i++) {
+        for (int p = 0; p < tl; p++) d[p] = node_distance(g, gc, i, p);
+        uint16_t* row = near.data() + (size_t)i * tl;
+        for (int p = 0; p < tl; p++) row[p] = (uint16_t)p;
+        std::sort(row, row + tl, [&](uint16_t a, uint16_t b) { return d[a] < d[b] || (d[a] == d[b] && a < b); });
+    }
+    return near;
+}
+
 bool decide_palette(const GridParams& g, const GroupCenters& gc, const unsigned* hist, long n_hsv,
-                    const phd_config& cfg, PaletteDecision* out) {
+                    const phd_config& cfg, PaletteDecision* out, const uint16_t* near) {
     const int tl = g.tl;
     const int L = cfg.linked_list_size;
-    // ---- ordering by saliency (insertion sort, swap while compare < 0)
+    // ---- ordering by saliency: custom_sort's insertion sort (swap while
+    // compare < 0).  x moves left past its neighbours while moves_past holds,
+    // so its place is the first neighbour, scanning left, where it fails.  The
+    // sorted prefix is a list of blocks (<= 2 kBlk entries, saliency max/min
+    // each): a block whose max or min alone shows that x moves past all of it
+    // (fl(y - x) is monotone in y) is skipped whole, one block is scanned, and
+    // an insertion shifts one block, so nothing is O(tl^2) in memory traffic.
     std::vector<float> sal(tl);
     for (int i = 0; i < tl; i++)
         sal[i] = saliency(hist[i], gc.s[i], gc.v[i], cfg.quantity_weight, cfg.saturation_value_weight);
-    std::vector<int> order(tl);
-    for (int i = 0; i < tl; i++) order[i] = i;
-    for (int i = 1; i < tl; i++)
-        for (int j = i; j > 0 && compare(sal[order[j]], sal[order[j - 1]]) < 0; j--)
-            std::swap(order[j], order[j - 1]);
+    constexpr int kBlk = 16;
+    struct Blk {
+        int n = 0;
+        float mx = 0, mn = 0;
+        int id[2 * kBlk + 1];
+        float sv[2 * kBlk + 1];
+        void bounds() {
+            mx = mn = sv[0];
+            for (int t = 1; t < n; t++) mx = std::max(mx, sv[t]), mn = std::min(mn, sv[t]);
+        }
+    };
+    std::vector<Blk> pool(1);
+    pool.reserve(tl / kBlk + 2);
+    std::vector<int> blocks{0};                          // block order
+    for (int i = 0; i < tl; i++) {
+        const float x = sal[i];
+        int b = (int)blocks.size() - 1, pos = 0;         // insert at (blocks[b], pos)
+        for (; b >= 0; b--) {
+            const Blk& k = pool[blocks[b]];
+            // max <= x - 1: every y <= max moves; min >= x + 2^31: every y >= min moves
+            if (k.n == 0 || !(k.mx - x > -1.0f) || !(k.mn - x < 2147483648.0f)) continue;
+            int p = k.n;
+            while (p > 0 && moves_past(k.sv[p - 1], x)) p--;
+            if (p > 0) {
+                pos = p;
+                break;
+            }
+        }
+        if (b < 0) b = 0, pos = 0;                       // x goes to the front
+        Blk& k = pool[blocks[b]];
+        std::memmove(&k.id[pos + 1], &k.id[pos], sizeof(int) * (k.n - pos));
+        std::memmove(&k.sv[pos + 1], &k.sv[pos], sizeof(float) * (k.n - pos));
+        k.id[pos] = i;
+        k.sv[pos] = x;
+        if (k.n++ == 0) k.mx = k.mn = x;
+        else k.mx = std::max(k.mx, x), k.mn = std::min(k.mn, x);
+        if (k.n > 2 * kBlk) {                             // split: the upper half to a new block
+            pool.emplace_back();
+            Blk& a = pool[blocks[b]];
+            Blk& c2 = pool.back();
+            c2.n = a.n - kBlk;
+            std::memcpy(c2.id, a.id + kBlk, sizeof(int) * c2.n);
+            std::memcpy(c2.sv, a.sv + kBlk, sizeof(float) * c2.n);
+            a.n = kBlk;
+            a.bounds();
+            c2.bounds();
+            blocks.insert(blocks.begin() + b + 1, (int)pool.size() - 1);
+        }
+    }
+    std::vector<int> order;
+    order.reserve(tl);
+    for (int b : blocks) order.insert(order.end(), pool[b].id, pool[b].id + pool[b].n);
     int goal = (int)((double)n_hsv * cfg.coverage_thresh);
     int np = -1;
     for (int i = 0; i < tl; i++) {
@@ -220,22 +290,41 @@ bool decide_palette(const GridParams& g, const GroupCenters& gc, const unsigned*
         out->off[k] = 180 - gc.h[p];
     }
     std::vector<double> dist(np);
+    std::vector<int> slot_of(tl, -1);
+    for (int k = 0; k < np; k++) slot_of[out->parents[k]] = k;
     for (int i = 0; i < tl; i++) {
         if (hist[i] == 0 || is_parent[i]) continue;
         double best = (double)tl * tl;                    // :368
-        int nmin = 0;
-        for (int k = 0; k < np; k++) {
-            const double d = node_distance(g, gc, i, out->parents[k]);
-            if (d < best) {
-                best = d;
-                nmin = 1;
-            } else if (d == best) {
+        int nmin = 0, k = 0;
+        if (near) {
+            // the nearest parents are the first parents of i's distance order;
+            // ties are adjacent there: count them, keep the first in palette order
+            const uint16_t* row = near + (size_t)i * tl;
+            int a = 0;
+            while (slot_of[row[a]] < 0) a++;
+            best = node_distance(g, gc, i, row[a]);
+            k = slot_of[row[a]];
+            nmin = 1;
+            for (a++; a < tl; a++) {
+                const int p = row[a];
+                if (slot_of[p] < 0) continue;
+                if (node_distance(g, gc, i, p) != best) break;
                 nmin++;
+                k = std::min(k, slot_of[p]);
             }
-            dist[k] = d;
+        } else {
+            for (int kk = 0; kk < np; kk++) {
+                const double d = node_distance(g, gc, i, out->parents[kk]);
+                if (d < best) {
+                    best = d;
+                    nmin = 1;
+                } else if (d == best) {
+                    nmin++;
+                }
+                dist[kk] = d;
+            }
+            while (dist[k] != best) k++;                  // first nearest, valid_parents order
         }
-        int k = 0;
-        while (dist[k] != best) k++;                      // first nearest, valid_parents order
         const long n = hist[i];
         GroupRule& r = out->rules[i];
         r.slot = k;

@@ -359,7 +359,6 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipStreamSynchronize(c->fft2));
     PHD_HIP(hipStreamSynchronize(c->dl));
     const GridParams gp = make_grid(cfg);
-    const GroupCenters gc = make_centers(gp);
     const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
     const long n_hsv = hsv_count(height, width, ds);
     const int nchunks = (int)((n_hsv + kChunk - 1) / kChunk);
@@ -503,12 +502,13 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     std::vector<std::vector<double>> hsum(n);                // fused: host part of the slot sums
     int* h_ent = (int*)(hp + L.E_pin(n) + L.e_entries);
     int* h_ns = (int*)(hp + L.E_pin(n) + L.e_ns);
-    int n_ent = 0, max_slots = 1;
+    int n_ent = 0, max_slots = 1, max_per_img = 0;
     for (int i = 0; i < n; i++) {
         const unsigned* hist = (const unsigned*)(hp + L.A(i) + L.a_hist);
         uint8_t* b = hp + (size_t)n * (L.a_bytes + L.c_bytes) + (size_t)i * L.b_bytes;
         h_ns[i] = 0;
-        if (!decide_palette(gp, gc, hist, n_hsv, cfg, &dec[i])) {
+        if (!decide_palette(gp, cls->gc, hist, n_hsv, cfg, &dec[i],
+                            cls->near.empty() ? nullptr : cls->near.data())) {
             ok[i] = 0;
             GroupRule* r = (GroupRule*)(b + L.b_rules);     // no slot: pass 2 keeps nothing
             for (int g = 0; g < gp.tl; g++) r[g] = GroupRule{-1, 0, 0, 0, 0xFFFFFFFFu, 0u};
@@ -522,6 +522,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             h_ent[2 * n_ent + 1] = g;
             n_ent++;
         }
+        max_per_img = std::max(max_per_img, (int)dec[i].search.size());
         h_ns[i] = (int)dec[i].parents.size();
         max_slots = std::max(max_slots, h_ns[i]);
         if (fused) {
@@ -558,7 +559,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                                               (const unsigned short*)(dw + L.H(n, 0)), (long)L.chunk_bytes,
                                               (const GroupRule*)(dw + L.B(n, 0) + L.b_rules),
                                               (const double*)(dw + L.B(n, 0) + L.b_off), (long)L.b_bytes,
-                                              (double*)(dw + L.C(n, 0) + L.c_pal), (long)L.c_bytes, s2));
+                                              (double*)(dw + L.C(n, 0) + L.c_pal), (long)L.c_bytes, max_per_img, s2));
             c->prof.end(ps, s2);
         } else {
             ps = c->prof.begin(kPalSums, s2);
@@ -1046,6 +1047,56 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
     return 0;
 }
 
+// Image indices grouped by size (groups in order of first appearance, each in
+// index order), at most `cap` per group: one batched run per group.
+static std::vector<std::vector<int>> size_groups(const int* heights, const int* widths, int n, int cap) {
+    std::vector<std::vector<int>> g;
+    std::map<std::pair<int, int>, int> open;                  // size -> its group still filling
+    for (int i = 0; i < n; i++) {
+        const auto key = std::make_pair(heights[i], widths[i]);
+        auto it = open.find(key);
+        if (it == open.end() || (int)g[it->second].size() >= cap) {
+            open[key] = (int)g.size();
+            g.emplace_back();
+        }
+        g[open[key]].push_back(i);
+    }
+    return g;
+}
+
+// Device-resident images of any sizes (BASELINE config 5): one batched run
+// (K1, FFTs, palette tail, per-image read-back) per group of same-size images.
+extern "C" int phd_report_batch_device_mixed(const uint8_t* const* d_images, const int* heights, const int* widths,
+                                             int n_images, const phd_config* cfg, Full_Report_Data** out,
+                                             int* status, void* stream) {
+    clear_error();
+    if (!d_images || !heights || !widths || !cfg || !out || !status || n_images <= 0) {
+        set_error("phd_report_batch_device_mixed: bad arguments");
+        return -1;
+    }
+    Context* c = get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int fails = 0;
+    for (const auto& grp : size_groups(heights, widths, n_images, 64)) {
+        const int m = (int)grp.size();
+        std::vector<const uint8_t*> ptrs(m);
+        std::vector<Full_Report_Data*> o(m, nullptr);
+        std::vector<int> st(m, -1);
+        for (int k = 0; k < m; k++) ptrs[k] = d_images[grp[k]];
+        run_reports(c, ptrs.data(), m, heights[grp[0]], widths[grp[0]], *cfg, nullptr, o.data(), st.data(),
+                    (hipStream_t)stream);
+        for (int k = 0; k < m; k++) {
+            out[grp[k]] = o[k];
+            status[grp[k]] = st[k];
+            fails += st[k] != 0;
+        }
+    }
+    return fails;
+}
+
+// Host images of any sizes: each same-size group (<= 16) is uploaded into one
+// device staging buffer and reported as one batch.
 extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
                                    int n_images, const phd_config* cfg, Full_Report_Data** out, int* status) {
     clear_error();
@@ -1053,11 +1104,47 @@ extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heig
         set_error("phd_report_batch_u8: bad arguments");
         return -1;
     }
-    int fails = 0;
     for (int i = 0; i < n_images; i++) {
-        out[i] = report_from_host(images[i], heights[i], widths[i], 0, cfg, nullptr);
-        status[i] = out[i] ? 0 : -1;
-        fails += !out[i];
+        out[i] = nullptr;
+        status[i] = -1;
+        if (!images[i]) {
+            set_error("Error: Image pointer is NULL.");
+            return -1;
+        }
+    }
+    Context* c = get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    int fails = 0;
+    for (const auto& grp : size_groups(heights, widths, n_images, 16)) {
+        const int m = (int)grp.size(), h = heights[grp[0]], w = widths[grp[0]];
+        if (!precheck(h, w)) {
+            fails += m;
+            continue;
+        }
+        const size_t bytes = 3 * (size_t)w * h;
+        if (!ensure_device((void**)&c->d_stage, &c->stage_bytes, (size_t)m * bytes)) return -1;
+        std::vector<const uint8_t*> ptrs(m);
+        bool up = true;
+        for (int k = 0; k < m && up; k++) {
+            ptrs[k] = c->d_stage + (size_t)k * bytes;
+            const hipError_t e = hipMemcpyAsync((void*)ptrs[k], images[grp[k]], bytes, hipMemcpyHostToDevice,
+                                                c->stream);
+            if (e != hipSuccess) {
+                set_error(std::string("upload failed: ") + hipGetErrorString(e));
+                up = false;
+            }
+        }
+        std::vector<Full_Report_Data*> o(m, nullptr);
+        std::vector<int> st(m, -1);
+        if (up) run_reports(c, ptrs.data(), m, h, w, *cfg, nullptr, o.data(), st.data(), nullptr);
+        // the caller's buffers may be freed on return: drain the uploads
+        (void)hipStreamSynchronize(c->stream);
+        for (int k = 0; k < m; k++) {
+            out[grp[k]] = o[k];
+            status[grp[k]] = st[k];
+            fails += st[k] != 0;
+        }
     }
     return fails;
 }

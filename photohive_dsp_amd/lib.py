@@ -54,6 +54,10 @@ lib.phd_report_batch_device.restype = ctypes.c_int
 lib.phd_report_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_size_t, P(PhdConfig), P(P(Full_Report_Data)),
                                         P(ctypes.c_int), ctypes.c_void_p]
+lib.phd_report_batch_device_mixed.restype = ctypes.c_int
+lib.phd_report_batch_device_mixed.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.POINTER(PhdConfig), ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p]
 lib.phd_blur_batch_device.restype = ctypes.c_int
 lib.phd_blur_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                       ctypes.POINTER(PhdConfig), ctypes.POINTER(ctypes.c_double),

@@ -278,6 +278,27 @@ def test_mixed_size_host_batch():
         np.testing.assert_allclose(np.array(r.blur_profile.bins), o.bins, rtol=FLOAT_RTOL, atol=1e-12)
 
 
+def test_mixed_size_device_batch_groups():
+    """phd_report_batch_device_mixed (config 5): interleaved sizes, grouped into
+    batches per size, each report equal to the single-image device report."""
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import report_device, reports_device_mixed
+    shapes = [(512, 512), (480, 640), (512, 512), (720, 1280), (480, 640), (512, 512)]
+    imgs = [synth.make(("structured", "uniform", "dominant")[i % 3], h, w, 40 + i) for i, (h, w) in enumerate(shapes)]
+    ts = [torch.from_numpy(im).cuda() for im in imgs]
+    kw = dict(h_partitions=36, s_partitions=4, v_partitions=5)
+    reps = reports_device_mixed(ts, **kw)
+    for t, r in zip(ts, reps):
+        one = report_device(t[None].contiguous(), **kw)[0]
+        assert r.color_palette.group_ids == one.color_palette.group_ids
+        assert r.color_palette.quantities == one.color_palette.quantities
+        np.testing.assert_allclose(np.array(r.blur_profile.bins), np.array(one.blur_profile.bins), rtol=1e-12,
+                                   atol=1e-15)
+        assert r.sharpnesses == one.sharpnesses
+        assert r.blur_vectors == one.blur_vectors
+
+
 def test_rejections_return_null():
     phd, L, _ = _phd()
     for h, w in [(349, 350), (2001, 400), (400, 2001)]:
@@ -307,6 +328,26 @@ def test_full_size_4000x3000_against_oracle(kind, seed):
     np.testing.assert_array_equal(hist, o.hist)
     np.testing.assert_array_equal(parents, o.valid_parents)
     np.testing.assert_array_equal(kept, o.kept)
+    g = dict(stats=o.stats, average_saturation=np.array(o.average_saturation), valid_parents=o.valid_parents,
+             palette_pct=o.palette_pct, palette_hsv=o.palette_hsv, bins=o.bins, blur_angles=o.blur_angles,
+             blur_mags=o.blur_mags, angle_bin_size=np.array(o.angle_bin_size),
+             radius_bin_size=np.array(o.radius_bin_size))
+    assert_report_matches(rep, g)
+
+
+@pytest.mark.parametrize("shape,kind", [((2000, 3000), "structured"), ((3000, 2000), "dominant"),
+                                        ((4000, 6000), "structured"), ((6000, 4000), "uniform")])
+def test_config5_large_sizes_against_oracle(shape, kind):
+    """The large config-5 sizes (compile-time row plans 2000 / 3000 / 6000,
+    column plans 2000 / 4000 / 6000) at h/s/v 36/4/5: the whole report
+    against the CPU oracle."""
+    phd, L, _ = _phd()
+    from photohive_dsp_amd import synth
+    from oracle import oracle as orc
+    kw = dict(h_partitions=36, s_partitions=4, v_partitions=5)
+    img = synth.make(kind, shape[0], shape[1], 11)
+    rep = phd.get_report(img, **kw)
+    o = orc.report(img, fft_workers=8, **kw)
     g = dict(stats=o.stats, average_saturation=np.array(o.average_saturation), valid_parents=o.valid_parents,
              palette_pct=o.palette_pct, palette_hsv=o.palette_hsv, bins=o.bins, blur_angles=o.blur_angles,
              blur_mags=o.blur_mags, angle_bin_size=np.array(o.angle_bin_size),
