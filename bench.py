@@ -196,10 +196,11 @@ def config5(lib, last_error, n=512, iters=2):
 
 def algorithmic_bytes(kernel, h, w):
     """Bytes one launch must move: RGB8 reads of the pixel passes,
-    the fp64-complex half spectrum written by the row pass and read by the column pass."""
+    the fp64-complex half spectrum written by the row pass and read by the column
+    pass, which also reads the u16 polar-bin map (2 B per spectrum element)."""
     n, hwf = h * w, h * (w // 2 + 1)
     return {"hsv_stats": 3 * n, "palette_sums": 3 * n, "fft_rows": 3 * n + 16 * hwf,
-            "fft_cols": 16 * hwf}.get(kernel)
+            "fft_cols": 18 * hwf}.get(kernel)
 
 
 def main():
@@ -208,10 +209,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    torch.cuda.set_device(local)
+    # PHD_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on one
+    # GPU (RCCL refuses two ranks on one device); the driver's runs use nccl
+    backend = os.environ.get("PHD_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev = local % ndev if ndev else local
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     import photohive_dsp_amd  # noqa: F401
     from photohive_dsp_amd.core import make_config
     from photohive_dsp_amd.lib import last_error, lib
@@ -248,10 +257,13 @@ def main():
                 out[name] = {"total_ms": tot.value, "launches": cnt.value, "avg_us": 1000 * tot.value / cnt.value}
         return out
 
-    # warmup; with events on every kernel, to find the dominant one
-    lib.phd_profile_kernels(0 if args.no_kernel_events else (1 << len(KERNELS)) - 1)
-    for _ in range(max(1, args.warmup)):
+    # warmup; the last warmup step with events on every kernel, to find the
+    # dominant one in steady state
+    lib.phd_profile_kernels(0)
+    for _ in range(max(1, args.warmup) - 1):
         step()
+    lib.phd_profile_kernels(0 if args.no_kernel_events else (1 << len(KERNELS)) - 1)
+    step()
     warm = kernel_times()
     dom = max(warm, key=lambda k: warm[k]["total_ms"]) if warm else None
 
@@ -260,9 +272,9 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    # timed region: HIP events bracket only the dominant kernel's launches
-    # (bracketing every launch costs ~7% throughput)
-    lib.phd_profile_kernels(0 if dom is None else 1 << KERNELS.index(dom))
+    # timed region: HIP events bracket the dominant kernel's first launch of
+    # every step (bracketing every launch costs ~7% throughput)
+    lib.phd_profile_kernels(0 if dom is None else (1 << KERNELS.index(dom)) | (1 << 31))
     barrier()
     t0 = time.perf_counter()
     stage = [0.0] * 8
@@ -280,7 +292,7 @@ def main():
     # the single collective: max of wall time, sums of images / pixels (shard.py)
     from photohive_dsp_amd.shard import merge_counters
     elapsed, images, _ = merge_counters(elapsed, float(B * args.steps), float(B * args.steps * H * W),
-                                        device="cuda")
+                                        device="cuda" if backend == "nccl" else "cpu")
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
@@ -309,7 +321,8 @@ def main():
     line["roofline"] = None
     if dom in kern:
         # the palette passes take the whole batch in one launch, the FFT passes one image
-        per_launch = B * args.steps / kern[dom]["launches"]
+        # (from the last warmup step, whose every launch was bracketed)
+        per_launch = B / warm[dom]["launches"]
         ab = algorithmic_bytes(dom, H, W) * per_launch
         achieved = ab / (kern[dom]["avg_us"] * 1e-6) / 1e9
         traffic = None
@@ -324,7 +337,8 @@ def main():
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                             "traffic": traffic, "algorithmic_bytes_per_launch": ab,
                             "images_per_launch": per_launch,
-                            "avg_launch_us": round(kern[dom]["avg_us"], 2)}
+                            "avg_launch_us": round(kern[dom]["avg_us"], 2),
+                            "launches_timed": kern[dom]["launches"], "sampling": "first launch of each step"}
         line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
     if not args.no_config3 and world == 1:
         line["config3"] = config3(lib, last_error)

@@ -254,6 +254,9 @@ const BlurTable* get_table(Context* c, int height, int width, int nr, int na) {
 
 int KernelProfiler::begin(int k, hipStream_t st) {
     if (!(mask & (1u << k))) return -1;
+    if (mask & kFirstOnly)
+        for (int p : pending)
+            if (p == k) return -1;
     const size_t slot = pending.size();
     if (slot >= pool.size()) {
         hipEvent_t a, b;
