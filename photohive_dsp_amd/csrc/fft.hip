@@ -231,9 +231,16 @@ __device__ __forceinline__ void load_twiddles(double2* tw, const FftPlan& plan) 
 
 // LDS: [ W complex | twiddles (64 + n_hi) | k255 (256 doubles) ]
 template <int T, bool GEN>
-__global__ __launch_bounds__(T) void k_fft_rows(const uint8_t* __restrict__ img, int H, int W, FftPlan plan,
-                                                const unsigned long long* __restrict__ sums,
-                                                const double* __restrict__ k255g, double2* __restrict__ inter) {
+__global__ __launch_bounds__(T) void k_fft_rows(const uint8_t* __restrict__ img0,
+                                                const uint8_t* const* __restrict__ imgs, int H, int W, FftPlan plan,
+                                                const unsigned long long* __restrict__ sums0, long sums_stride,
+                                                const double* __restrict__ k255g, double2* __restrict__ inter0,
+                                                size_t inter_stride) {
+    // blockIdx.y: the image of a batch (imgs[y], sums0 + y * sums_stride u64,
+    // inter0 + y * inter_stride elements); imgs == nullptr: img0 alone
+    const uint8_t* img = imgs ? imgs[blockIdx.y] : img0;
+    const unsigned long long* sums = sums0 + (size_t)blockIdx.y * sums_stride;
+    double2* inter = inter0 + (size_t)blockIdx.y * inter_stride;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
     double2* tw = buf + W;
@@ -286,10 +293,15 @@ __global__ __launch_bounds__(T) void k_fft_rows(const uint8_t* __restrict__ img,
 
 // LDS: [ C*H complex | twiddles (64 + n_hi) | polar bins (nbins doubles, if lds_bins) ]
 template <int T, bool GEN>
-__global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inter, int H, int wf, int C,
-                                                FftPlan plan, const uint16_t* __restrict__ binmap, int nbins,
-                                                int lds_bins, double* __restrict__ bin_sums,
-                                                double* __restrict__ fmax_part, int ablate) {
+__global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inter0, size_t inter_stride, int H,
+                                                int wf, int C, FftPlan plan, const uint16_t* __restrict__ binmap,
+                                                int nbins, int lds_bins, double* __restrict__ bin_sums0,
+                                                double* __restrict__ fmax_part0, long out_stride, int ablate) {
+    // blockIdx.y: the image of a batch (inter0 + y * inter_stride elements,
+    // bin sums and max partials at + y * out_stride doubles)
+    const double2* inter = inter0 + (size_t)blockIdx.y * inter_stride;
+    double* bin_sums = bin_sums0 + (size_t)blockIdx.y * out_stride;
+    double* fmax_part = fmax_part0 + (size_t)blockIdx.y * out_stride;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
     double2* tw = buf + (size_t)C * H;
@@ -362,35 +374,52 @@ static void allow_big_lds(K kernel) {
 }
 
 template <int T, bool GEN>
-static hipError_t rows_impl(const uint8_t* img, int height, int width, const FftPlan& plan,
-                            const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st) {
+static hipError_t rows_impl(const uint8_t* img, const uint8_t* const* imgs, int n, int height, int width,
+                            const FftPlan& plan, const unsigned long long* sums, long sums_stride, const double* k255,
+                            double2* inter, size_t inter_stride, hipStream_t st) {
     static bool once = (allow_big_lds(k_fft_rows<T, GEN>), true);
     (void)once;
     const size_t lds = sizeof(double2) * (width + 64 + plan.n_hi) + 256 * sizeof(double);
-    hipLaunchKernelGGL((k_fft_rows<T, GEN>), dim3((height + 1) / 2), dim3(T), lds, st, img, height, width, plan,
-                       sums, k255, inter);
+    hipLaunchKernelGGL((k_fft_rows<T, GEN>), dim3((height + 1) / 2, n), dim3(T), lds, st, img, imgs, height, width,
+                       plan, sums, sums_stride, k255, inter, inter_stride);
     return hipGetLastError();
+}
+
+template <bool GEN>
+static hipError_t rows_t(const uint8_t* img, const uint8_t* const* imgs, int n, int height, int width,
+                         const FftPlan& plan, const unsigned long long* sums, long sums_stride, const double* k255,
+                         double2* inter, size_t inter_stride, hipStream_t st) {
+    if (width <= 4096)
+        return rows_impl<512, GEN>(img, imgs, n, height, width, plan, sums, sums_stride, k255, inter, inter_stride, st);
+    return rows_impl<1024, GEN>(img, imgs, n, height, width, plan, sums, sums_stride, k255, inter, inter_stride, st);
+}
+
+hipError_t launch_fft_rows_batch(const uint8_t* const* d_imgs, int n, int height, int width, const FftPlan& plan,
+                                 const unsigned long long* sums0, long sums_stride, const double* k255,
+                                 double2* inter0, size_t inter_stride, hipStream_t st) {
+    return plan.generic
+                   ? rows_t<true>(nullptr, d_imgs, n, height, width, plan, sums0, sums_stride, k255, inter0,
+                                  inter_stride, st)
+                   : rows_t<false>(nullptr, d_imgs, n, height, width, plan, sums0, sums_stride, k255, inter0,
+                                   inter_stride, st);
 }
 
 hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftPlan& plan,
                            const unsigned long long* sums, const double* k255, double2* inter,
                            hipStream_t st) {
-    if (width <= 4096)
-        return plan.generic ? rows_impl<512, true>(img, height, width, plan, sums, k255, inter, st)
-                            : rows_impl<512, false>(img, height, width, plan, sums, k255, inter, st);
-    return plan.generic ? rows_impl<1024, true>(img, height, width, plan, sums, k255, inter, st)
-                        : rows_impl<1024, false>(img, height, width, plan, sums, k255, inter, st);
+    return plan.generic ? rows_t<true>(img, nullptr, 1, height, width, plan, sums, 0, k255, inter, 0, st)
+                        : rows_t<false>(img, nullptr, 1, height, width, plan, sums, 0, k255, inter, 0, st);
 }
 
 template <int T, bool GEN>
-static hipError_t cols_impl(const double2* inter, int height, int wf, int C, const FftPlan& plan,
-                            const uint16_t* binmap, int nbins, int lds_bins, size_t lds, double* bin_sums,
-                            double* fmax_part, hipStream_t st) {
+static hipError_t cols_impl(const double2* inter, size_t inter_stride, int n, int height, int wf, int C,
+                            const FftPlan& plan, const uint16_t* binmap, int nbins, int lds_bins, size_t lds,
+                            double* bin_sums, double* fmax_part, long out_stride, hipStream_t st) {
     static bool once = (allow_big_lds(k_fft_cols<T, GEN>), true);
     (void)once;
     static const int ablate = getenv("PHD_ABLATE") ? atoi(getenv("PHD_ABLATE")) : 0;   // debug only
-    hipLaunchKernelGGL((k_fft_cols<T, GEN>), dim3((wf + C - 1) / C), dim3(T), lds, st, inter, height, wf, C, plan,
-                       binmap, nbins, lds_bins, bin_sums, fmax_part, ablate);
+    hipLaunchKernelGGL((k_fft_cols<T, GEN>), dim3((wf + C - 1) / C, n), dim3(T), lds, st, inter, inter_stride, height,
+                       wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_part, out_stride, ablate);
     return hipGetLastError();
 }
 
@@ -408,17 +437,33 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     return C;
 }
 
-hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
-                           const uint16_t* binmap, int nbins, double* bin_sums,
-                           double* fmax_part, hipStream_t st) {
+template <bool GEN>
+static hipError_t cols_t(const double2* inter0, size_t inter_stride, int n, int height, int wf, const FftPlan& plan,
+                         const uint16_t* binmap, int nbins, double* bin_sums0, double* fmax_part0, long out_stride,
+                         hipStream_t st) {
     size_t lds;
     int lds_bins;
     const int C = fft_cols_blocks(height, wf, nbins, plan, &lds, &lds_bins);
     if ((size_t)C * height <= 4096)
-        return plan.generic ? cols_impl<512, true>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st)
-                            : cols_impl<512, false>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st);
-    return plan.generic ? cols_impl<1024, true>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st)
-                        : cols_impl<1024, false>(inter, height, wf, C, plan, binmap, nbins, lds_bins, lds, bin_sums, fmax_part, st);
+        return cols_impl<512, GEN>(inter0, inter_stride, n, height, wf, C, plan, binmap, nbins, lds_bins, lds,
+                                   bin_sums0, fmax_part0, out_stride, st);
+    return cols_impl<1024, GEN>(inter0, inter_stride, n, height, wf, C, plan, binmap, nbins, lds_bins, lds,
+                                bin_sums0, fmax_part0, out_stride, st);
+}
+
+hipError_t launch_fft_cols_batch(const double2* inter0, size_t inter_stride, int n, int height, int wf,
+                                 const FftPlan& plan, const uint16_t* binmap, int nbins, double* bin_sums0,
+                                 double* fmax_part0, long out_stride, hipStream_t st) {
+    return plan.generic ? cols_t<true>(inter0, inter_stride, n, height, wf, plan, binmap, nbins, bin_sums0,
+                                       fmax_part0, out_stride, st)
+                        : cols_t<false>(inter0, inter_stride, n, height, wf, plan, binmap, nbins, bin_sums0,
+                                        fmax_part0, out_stride, st);
+}
+
+hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
+                           const uint16_t* binmap, int nbins, double* bin_sums,
+                           double* fmax_part, hipStream_t st) {
+    return launch_fft_cols_batch(inter, 0, 1, height, wf, plan, binmap, nbins, bin_sums, fmax_part, 0, st);
 }
 
 }  // namespace phd

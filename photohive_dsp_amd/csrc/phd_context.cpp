@@ -6,6 +6,8 @@
 #include <cstdio>
 #include <cstring>
 
+#include <thread>
+
 #include "phd_host.h"
 
 namespace phd {
@@ -250,6 +252,53 @@ const BlurTable* get_table(Context* c, int height, int width, int nr, int na) {
     BlurTable t;
     if (!build_blur_table(height, width, nr, na, &t)) return nullptr;
     return &(c->tables[key] = std::move(t));
+}
+
+HostPool::HostPool(int threads) : nthreads_(threads) {
+    for (int t = 0; t < threads; t++) std::thread([this] { worker(); }).detach();
+}
+
+void HostPool::worker() {
+    unsigned seen = 0;
+    for (;;) {
+        const std::function<void(int)>* fn;
+        int n;
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            cv_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            fn = fn_;
+            n = n_;
+        }
+        for (int i; (i = next_.fetch_add(1)) < n;) (*fn)(i);
+        std::lock_guard<std::mutex> lk(m_);
+        if (--busy_ == 0) done_.notify_one();
+    }
+}
+
+void HostPool::parallel_for(int n, const std::function<void(int)>& f) {
+    {
+        std::lock_guard<std::mutex> lk(m_);
+        fn_ = &f;
+        n_ = n;
+        next_.store(0);
+        busy_ = nthreads_;
+        gen_++;
+    }
+    cv_.notify_all();
+    for (int i; (i = next_.fetch_add(1)) < n;) f(i);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return busy_ == 0; });
+    fn_ = nullptr;
+}
+
+HostPool* host_pool() {
+    static HostPool* p = [] {
+        const unsigned hc = std::thread::hardware_concurrency();
+        const int t = hc > 1 ? (int)std::min(hc - 1, 7u) : 0;
+        return new HostPool(t);
+    }();
+    return p;
 }
 
 int KernelProfiler::begin(int k, hipStream_t st) {

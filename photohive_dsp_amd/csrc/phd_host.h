@@ -1,6 +1,9 @@
 // phd_host.h -- host-side internals of libreport_data.so (C++17).
 #pragma once
 
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -97,6 +100,27 @@ struct KernelProfiler {
 };
 
 // ---- device context ---------------------------------------------------------
+// A few persistent host threads for the per-image host work of a batch (the
+// palette decisions): parallel_for(n, f) runs f(0 .. n-1) on them and on the
+// caller.  The threads are detached and the pool is never destroyed.
+class HostPool {
+public:
+    explicit HostPool(int threads);
+    void parallel_for(int n, const std::function<void(int)>& f);
+    int size() const { return nthreads_; }
+
+private:
+    void worker();
+    int nthreads_ = 0;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* fn_ = nullptr;
+    std::atomic<int> next_{0};
+    int n_ = 0, busy_ = 0;
+    unsigned gen_ = 0;
+};
+HostPool* host_pool();
+
 struct Context {
     int device = -1;
     hipStream_t stream = nullptr;

@@ -176,6 +176,17 @@ hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds
                                const double* k255, hipStream_t st);
 // Row pass: luma - avg of two rows as one complex sequence, FFT, split, write
 // the half spectra column-major into inter[wf][height].
+// Runtime-plan FFT passes over a batch of same-size images in one launch each
+// (grid.y = image): image y's pixels d_imgs[y] (device array), channel sums
+// at sums0 + y * sums_stride, intermediate at inter0 + y * inter_stride
+// elements; the column pass's bin sums and max partials at + y * out_stride
+// doubles.
+hipError_t launch_fft_rows_batch(const uint8_t* const* d_imgs, int n, int height, int width, const FftPlan& plan,
+                                 const unsigned long long* sums0, long sums_stride, const double* k255,
+                                 double2* inter0, size_t inter_stride, hipStream_t st);
+hipError_t launch_fft_cols_batch(const double2* inter0, size_t inter_stride, int n, int height, int wf,
+                                 const FftPlan& plan, const uint16_t* binmap, int nbins, double* bin_sums0,
+                                 double* fmax_part0, long out_stride, hipStream_t st);
 hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftPlan& plan,
                            const unsigned long long* sums, const double* k255,
                            double2* inter, hipStream_t st);

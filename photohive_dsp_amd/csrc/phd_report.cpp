@@ -388,7 +388,13 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // images/s at 4000x3000: the two 96 MB intermediates no longer share the
     // MALL with the pixels), so the FFTs run serially on one stream by default.
     static const bool pipe_env = getenv("PHD_FFT_PIPE") != nullptr;
-    const bool pipe = Q == 1 && n > 1 && pipe_env;
+    // runtime-plan sizes: the passes of a group of images are one launch each
+    // (grid.y = image), the group's intermediates within 128 MB (half the
+    // MALL); small images are otherwise bound by per-launch latency
+    static const bool gbatch_off = getenv("PHD_FFT_NO_BATCH") != nullptr;
+    const bool gbatch = !fs.ct && !gbatch_off && n > 1 && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
+    if (gbatch) Q = std::max(1, std::min(n, (int)(((size_t)128 << 20) / inter_one)));
+    const bool pipe = !gbatch && Q == 1 && n > 1 && pipe_env;
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)(pipe ? 2 : Q) * inter_one))
         return false;
@@ -459,7 +465,29 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             PHD_HIP(hipEventRecord(c->ev_img_fft[i], sc));
         }
     }
-    for (int g0 = 0; g0 < (pipe ? 0 : n); g0 += Q) {
+    for (int g0 = 0; gbatch && g0 < n; g0 += Q) {
+        const int g1 = std::min(n, g0 + Q);
+        const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(n));
+        int ps = c->prof.begin(kFftRows, sf);
+        PHD_HIP(launch_fft_rows_batch(d_ptrs + g0, g1 - g0, height, width, fs.prow->plan,
+                                      (const unsigned long long*)(dw + L.A(g0) + L.a_sums), (long)(L.a_bytes / 8),
+                                      c->d_k255, c->d_inter, inter_elems, sf));
+        c->prof.end(ps, sf);
+        ps = c->prof.begin(kFftCols, sf);
+        PHD_HIP(launch_fft_cols_batch(c->d_inter, inter_elems, g1 - g0, height, wf, fs.pcol->plan, tbl->d_map, nbins,
+                                      (double*)(dw + L.C(n, g0) + L.c_bins), (double*)(dw + L.C(n, g0) + L.c_fmax),
+                                      (long)(L.c_bytes / 8), sf));
+        c->prof.end(ps, sf);
+        for (int i = g0; i < g1; i++) {
+            if (ncrops)
+                PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
+                                         crop_arr.data() + ncrops, crop_arr.data() + 2 * ncrops,
+                                         crop_arr.data() + 3 * ncrops, c->d_k255,
+                                         (double*)(dw + L.C(n, i) + L.c_sharp), sf));
+            PHD_HIP(hipEventRecord(c->ev_img_fft[i], sf));
+        }
+    }
+    for (int g0 = 0; g0 < (pipe || gbatch ? 0 : n); g0 += Q) {
         const int g1 = std::min(n, g0 + Q);
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
@@ -503,20 +531,45 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     int* h_ent = (int*)(hp + L.E_pin(n) + L.e_entries);
     int* h_ns = (int*)(hp + L.E_pin(n) + L.e_ns);
     int n_ent = 0, max_slots = 1, max_per_img = 0;
-    for (int i = 0; i < n; i++) {
+    // per image, independent: the decision, its device records and (fused) the
+    // host part of the slot sums; on the host pool when the decisions are
+    // costly (fine grids), then the batch-wide lists in image order
+    std::vector<std::string> fail_why(n);
+    auto decide_one = [&](int i) {
         const unsigned* hist = (const unsigned*)(hp + L.A(i) + L.a_hist);
         uint8_t* b = hp + (size_t)n * (L.a_bytes + L.c_bytes) + (size_t)i * L.b_bytes;
-        h_ns[i] = 0;
         if (!decide_palette(gp, cls->gc, hist, n_hsv, cfg, &dec[i],
                             cls->near.empty() ? nullptr : cls->near.data())) {
             ok[i] = 0;
             GroupRule* r = (GroupRule*)(b + L.b_rules);     // no slot: pass 2 keeps nothing
             for (int g = 0; g < gp.tl; g++) r[g] = GroupRule{-1, 0, 0, 0, 0xFFFFFFFFu, 0u};
-            continue;
+            return;
         }
         memcpy(b + L.b_rules, dec[i].rules.data(), sizeof(GroupRule) * gp.tl);
         memcpy(b + L.b_search, dec[i].search.data(), sizeof(int) * dec[i].search.size());
         memcpy(b + L.b_off, dec[i].off.data(), sizeof(double) * dec[i].off.size());
+        if (fused) {
+            hsum[i].assign(4 * dec[i].parents.size(), 0.0);
+            if (!fused_slot_sums(gp, dec[i], hist, (const double*)(hp + L.A(i) + L.a_gsum),
+                                 (const unsigned*)(hp + L.A(i) + L.a_gcell), hsum[i].data(), &fail_why[i]))
+                ok[i] = 0;
+        }
+    };
+    HostPool* pool = host_pool();
+    if (n >= 4 && gp.tl >= 200 && pool->size() > 0) pool->parallel_for(n, decide_one);
+    else
+        for (int i = 0; i < n; i++) decide_one(i);
+    for (int i = 0; i < n; i++) {
+        h_ns[i] = 0;
+        if (!ok[i]) {
+            // the message, on this thread (decide_palette is deterministic)
+            if (!fail_why[i].empty()) set_error(fail_why[i]);
+            else {
+                PaletteDecision d;
+                (void)decide_palette(gp, cls->gc, (const unsigned*)(hp + L.A(i) + L.a_hist), n_hsv, cfg, &d);
+            }
+            continue;
+        }
         for (int g : dec[i].search) {
             h_ent[2 * n_ent] = i;
             h_ent[2 * n_ent + 1] = g;
@@ -525,15 +578,6 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         max_per_img = std::max(max_per_img, (int)dec[i].search.size());
         h_ns[i] = (int)dec[i].parents.size();
         max_slots = std::max(max_slots, h_ns[i]);
-        if (fused) {
-            hsum[i].assign(4 * dec[i].parents.size(), 0.0);
-            std::string w;
-            if (!fused_slot_sums(gp, dec[i], hist, (const double*)(hp + L.A(i) + L.a_gsum),
-                                 (const unsigned*)(hp + L.A(i) + L.a_gcell), hsum[i].data(), &w)) {
-                set_error(w);
-                ok[i] = 0;
-            }
-        }
     }
     // the second pass on the tail stream, after K1, concurrent with the FFTs
     const hipStream_t s2 = c->tail;

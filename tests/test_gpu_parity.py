@@ -299,6 +299,27 @@ def test_mixed_size_device_batch_groups():
         assert r.blur_vectors == one.blur_vectors
 
 
+@pytest.mark.parametrize("shape", [(720, 1280), (513, 700)])
+def test_runtime_plan_batch_against_oracle(shape):
+    """Runtime-plan sizes in a batch: the row and column passes of the batch are
+    one launch each (grid.y = image); every image's report against the CPU
+    oracle."""
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import report_device
+    from oracle import oracle as orc
+    h, w = shape
+    imgs = np.stack([synth.make(("structured", "uniform", "dominant")[i % 3], h, w, 60 + i) for i in range(5)])
+    reps = report_device(torch.from_numpy(imgs).cuda())
+    for img, rep in zip(imgs, reps):
+        o = orc.report(img)
+        g = dict(stats=o.stats, average_saturation=np.array(o.average_saturation), valid_parents=o.valid_parents,
+                 palette_pct=o.palette_pct, palette_hsv=o.palette_hsv, bins=o.bins, blur_angles=o.blur_angles,
+                 blur_mags=o.blur_mags, angle_bin_size=np.array(o.angle_bin_size),
+                 radius_bin_size=np.array(o.radius_bin_size))
+        assert_report_matches(rep, g)
+
+
 def test_rejections_return_null():
     phd, L, _ = _phd()
     for h, w in [(349, 350), (2001, 400), (400, 2001)]:
