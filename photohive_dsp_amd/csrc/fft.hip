@@ -380,7 +380,7 @@ static hipError_t rows_impl(const uint8_t* img, const uint8_t* const* imgs, int 
     static bool once = (allow_big_lds(k_fft_rows<T, GEN>), true);
     (void)once;
     const size_t lds = sizeof(double2) * (width + 64 + plan.n_hi) + 256 * sizeof(double);
-    hipLaunchKernelGGL((k_fft_rows<T, GEN>), dim3((height + 1) / 2, n), dim3(T), lds, st, img, imgs, height, width,
+    phd_launch((k_fft_rows<T, GEN>), dim3((height + 1) / 2, n), dim3(T), lds, st, img, imgs, height, width,
                        plan, sums, sums_stride, k255, inter, inter_stride);
     return hipGetLastError();
 }
@@ -418,7 +418,7 @@ static hipError_t cols_impl(const double2* inter, size_t inter_stride, int n, in
     static bool once = (allow_big_lds(k_fft_cols<T, GEN>), true);
     (void)once;
     static const int ablate = getenv("PHD_ABLATE") ? atoi(getenv("PHD_ABLATE")) : 0;   // debug only
-    hipLaunchKernelGGL((k_fft_cols<T, GEN>), dim3((wf + C - 1) / C, n), dim3(T), lds, st, inter, inter_stride, height,
+    phd_launch((k_fft_cols<T, GEN>), dim3((wf + C - 1) / C, n), dim3(T), lds, st, inter, inter_stride, height,
                        wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_part, out_stride, ablate);
     return hipGetLastError();
 }

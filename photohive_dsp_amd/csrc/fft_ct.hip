@@ -448,7 +448,7 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
         const int g = resident_grid(k_rows_ct<W, T, Rs...>, T, lds) / 32 * 32;   // schedule needs % 32
         return g > 32 ? g : 32;
     }();
-    hipLaunchKernelGGL((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
+    phd_launch((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
                        g_ablate, rsum);
     return hipGetLastError();
 }
@@ -467,7 +467,7 @@ hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binm
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st) {
     const size_t lds = ColK<H, T, CPB, Rs...>::lds(nbins);
-    hipLaunchKernelGGL((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3((CPB & 3) * T), lds,
+    phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3((CPB & 3) * T), lds,
                        st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, g_ablate);
     return hipGetLastError();
 }

@@ -515,7 +515,7 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
         attr = true;
     }
     const int grid = (int)std::min<long>(nitems, (long)num_cus());
-    hipLaunchKernelGGL(k_k1t, dim3(grid), dim3(kT), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255, out0,
+    phd_launch(k_k1t, dim3(grid), dim3(kT), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255, out0,
                        a_stride, h_stride, cshift, env_ablate());
     return hipGetLastError();
 }

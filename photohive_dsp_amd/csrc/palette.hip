@@ -1462,14 +1462,14 @@ hipError_t launch_hsv_ds(const uint8_t* img, int height, int width, int ds, cons
     const long n = hsv_pixels(height, width, ds, &nw);
     const size_t lds = K1Lds::area + sizeof(unsigned) * ((gp.tl + 3) & ~3);
     if (fc.use_thr)
-        hipLaunchKernelGGL(k_hsv_ds<true>, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
+        phd_launch(k_hsv_ds<true>, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
                            tabs, k255, out);
     else
-        hipLaunchKernelGGL(k_hsv_ds<false>, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
+        phd_launch(k_hsv_ds<false>, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw, gp, fc,
                            tabs, k255, out);
     const long nbytes = 3L * height * width;
     const int blocks = (int)std::min<long>(2048, (nbytes / 3 + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_stats, dim3(blocks), dim3(kThreads), 0, st, img, nbytes, out.sums);
+    phd_launch(k_stats, dim3(blocks), dim3(kThreads), 0, st, img, nbytes, out.sums);
     return hipGetLastError();
 }
 
@@ -1480,7 +1480,7 @@ hipError_t launch_palette_cutoffs(const uint8_t* img, int height, int width, int
     if (n_search <= 0) return hipSuccess;
     int nw;
     const long n = hsv_pixels(height, width, ds, &nw);
-    hipLaunchKernelGGL(k_cutoffs, dim3(n_search), dim3(kThreads), 0, st, img, n, width, ds, nw, gp,
+    phd_launch(k_cutoffs, dim3(n_search), dim3(kThreads), 0, st, img, n, width, ds, nw, gp,
                        chunk_hist, nchunks, rules, search_groups, k255);
     return hipGetLastError();
 }
@@ -1493,7 +1493,7 @@ hipError_t launch_palette_sums(const uint8_t* img, int height, int width, int ds
     const int nchunks = (int)((n + kChunk - 1) / kChunk);
     const size_t lds = sizeof(double) * (256 + 5 * (size_t)nslots) + sizeof(GroupRule) * gp.tl;
     const int aligned = (reinterpret_cast<uintptr_t>(img) & 3) == 0;
-    hipLaunchKernelGGL(k_palette_sums, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw,
+    phd_launch(k_palette_sums, dim3(nchunks), dim3(kThreads), lds, st, img, n, width, ds, nw,
                        gp, rules, slot_off, nslots, out, k255, aligned);
     return hipGetLastError();
 }
@@ -1522,7 +1522,7 @@ hipError_t launch_cutoffs_batch(const uint8_t* const* d_imgs, const uint8_t* con
                                       160 * 1024);                                                          \
             attr = true;                                                                                    \
         }                                                                                                   \
-        hipLaunchKernelGGL((k_cutoffs_b<A, T>), dim3(n_entries), dim3(kK1Threads), lds, st, d_imgs, npix,        \
+        phd_launch((k_cutoffs_b<A, T>), dim3(n_entries), dim3(kK1Threads), lds, st, d_imgs, npix,        \
                            nchunks, gp, fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, b_stride);  \
     } while (0)
     if (fc.use_thr) {
@@ -1564,7 +1564,7 @@ hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              \
             attr = true;                                                                                    \
         }                                                                                                   \
-        hipLaunchKernelGGL((k_palette_sums_b<A, T>), dim3(grid), dim3(kK3Threads), lds, st, d_imgs, npix,        \
+        phd_launch((k_palette_sums_b<A, T>), dim3(grid), dim3(kK3Threads), lds, st, d_imgs, npix,        \
                            nchunks, nitems, gp, fc, tabs, k255, rules0, off0, b_stride, nslots_img,         \
                            max_slots, out0, c_stride, k3_cshift(max_slots), env_ablate());                  \
     } while (0)
@@ -1594,7 +1594,7 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
         const size_t lds = PartImgLds::bytes(gp.tl);
         const dim3 grid(n, 64);
 #define PHD_PI_LAUNCH(A, T)                                                                                     \
-    hipLaunchKernelGGL((k_partial_sums_img<A, T>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc, tabs, \
+    phd_launch((k_partial_sums_img<A, T>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc, tabs, \
                        k255, entries, n_entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride)
         if (fc.use_thr) {
             if (aligned) PHD_PI_LAUNCH(true, true);
@@ -1610,17 +1610,17 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     const dim3 grid(n_entries, 32);
     if (fc.use_thr) {
         if (aligned)
-            hipLaunchKernelGGL((k_partial_sums_b<true, true>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc,
+            phd_launch((k_partial_sums_b<true, true>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc,
                                tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
         else
-            hipLaunchKernelGGL((k_partial_sums_b<false, true>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
+            phd_launch((k_partial_sums_b<false, true>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
                                fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
     } else {
         if (aligned)
-            hipLaunchKernelGGL((k_partial_sums_b<true, false>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
+            phd_launch((k_partial_sums_b<true, false>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
                                fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
         else
-            hipLaunchKernelGGL((k_partial_sums_b<false, false>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
+            phd_launch((k_partial_sums_b<false, false>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp,
                                fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride);
     }
     return hipGetLastError();
@@ -1629,16 +1629,16 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st) {
     if (fc.use_thr)
-        hipLaunchKernelGGL(k_debug_hsv<true>, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
+        phd_launch(k_debug_hsv<true>, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
     else
-        hipLaunchKernelGGL(k_debug_hsv<false>, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
+        phd_launch(k_debug_hsv<false>, dim3(2048), dim3(256), 0, st, img, n, gp, fc, tabs, k255, gid, hsv);
     return hipGetLastError();
 }
 
 hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st) {
     const size_t nw = (n + 7) / 8;
     const int blocks = (int)std::min<size_t>(4096, (nw + 255) / 256);
-    hipLaunchKernelGGL(k_fill_uniform, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, dst, n,
+    phd_launch(k_fill_uniform, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, dst, n,
                        (unsigned long long)seed);
     return hipGetLastError();
 }

@@ -303,9 +303,8 @@ HostPool* host_pool() {
 
 int KernelProfiler::begin(int k, hipStream_t st) {
     if (!(mask & (1u << k))) return -1;
-    if (mask & kFirstOnly)
-        for (int p : pending)
-            if (p == k) return -1;
+    const unsigned stride = (mask >> 24) & 127u;
+    if (stride > 1 && calls % stride != 0) return -1;
     const size_t slot = pending.size();
     if (slot >= pool.size()) {
         hipEvent_t a, b;
@@ -313,16 +312,25 @@ int KernelProfiler::begin(int k, hipStream_t st) {
         pool.emplace_back(a, b);
     }
     pending.push_back(k);
-    (void)hipEventRecord(pool[slot].first, st);
+    launch_events() = LaunchEvents{pool[slot].first, pool[slot].second, false};
     return (int)slot;
 }
 
 void KernelProfiler::end(int slot, hipStream_t st) {
-    if (slot >= 0) (void)hipEventRecord(pool[slot].second, st);
+    if (slot < 0) return;
+    if (!launch_events().used) pending[slot] = -1;   // no phd_launch took the events
+    launch_events() = LaunchEvents{};
+}
+
+LaunchEvents& launch_events() {
+    static thread_local LaunchEvents e;
+    return e;
 }
 
 void KernelProfiler::collect() {
+    calls++;
     for (size_t i = 0; i < pending.size(); i++) {
+        if (pending[i] < 0) continue;
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, pool[i].first, pool[i].second) == hipSuccess) {
             total_ms[pending[i]] += ms;
@@ -356,6 +364,7 @@ extern "C" int phd_profile_kernels(unsigned mask) {
     if (!c) return -1;
     std::lock_guard<std::mutex> lk(c->mu);
     c->prof.mask = mask;
+    c->prof.calls = 0;
     c->prof.pending.clear();
     for (int k = 0; k < phd::kNumKernels; k++) {
         c->prof.total_ms[k] = 0.0;

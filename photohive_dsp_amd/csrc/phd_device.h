@@ -7,6 +7,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 // Ablation switches for timing experiments exist only in builds made with
 // -DPHD_ABLATE_BUILD (a separate library, tools/); in the product they are 0.
@@ -21,6 +22,18 @@
 #include "phd_internal.h"
 
 namespace phd {
+
+// Every kernel launch of the library: a profiled launch (launch_events set)
+// records the profiler's events with the dispatch itself.
+template <typename F, typename... Args>
+inline void phd_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
+    LaunchEvents& e = launch_events();
+    const bool timed = e.start != nullptr && !e.used;
+    hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, timed ? e.start : nullptr,
+                          timed ? e.stop : nullptr, 0u, args...);
+    if (timed) e.used = true;
+}
+
 
 // rgb2hsv for one pixel (src/image_processing.c:387-414).  The inputs are the
 // doubles k/255.0 of the reference's planar image (utils.py:30-46).

@@ -86,11 +86,12 @@ bool make_fft_plan(int n, FftPlanHost* p);
 enum KernelId { kK1 = 0, kFftRows = 1, kFftCols = 2, kCutoffs = 3, kPalSums = 4, kSharp = 5, kNumKernels = 6 };
 struct KernelProfiler {
     unsigned mask = 0;                              // kernels to bracket with events
-    // mask bit 31: only the first launch of each kernel per batch call (the
-    // events between back-to-back launches cost ~7% of a batch's time)
-    static constexpr unsigned kFirstOnly = 1u << 31;
+    // mask bits 24-30: stride s > 1, only every s-th batch call is bracketed
+    // (all its launches; the events between back-to-back launches cost ~6% of
+    // a bracketed call's time)
+    unsigned calls = 0;                             // batch calls since the mask was set
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
-    std::vector<int> pending;                       // kernel id per used pair
+    std::vector<int> pending;                       // kernel id per used pair (-1: launch not timed)
     double total_ms[kNumKernels] = {};
     long launches[kNumKernels] = {};
     // record the opening event of a launch of kernel k (no-op unless enabled)

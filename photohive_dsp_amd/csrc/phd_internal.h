@@ -10,6 +10,17 @@
 
 namespace phd {
 
+// Events that the next profiled launch records as part of its own dispatch
+// (hipExtLaunchKernel: the kernel's start and end, no event packets between
+// back-to-back kernels).  KernelProfiler::begin sets them; phd_launch uses
+// them once.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+    bool used = false;
+};
+LaunchEvents& launch_events();   // thread-local
+
+
 // Pixels per palette chunk: the unit of work of the hsv/stats kernel and the
 // palette-sums kernel, and the granularity of the per-chunk group histograms
 // the tie-overflow cutoff search walks (counts fit uint16).

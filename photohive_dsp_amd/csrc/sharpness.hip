@@ -77,9 +77,9 @@ hipError_t launch_sharpness(const uint8_t* img, int height, int width, int n, co
         const int cw = right[k] - left[k], ch = bottom[k] - top[k];
         const long cn = (long)cw * ch;
         const int blocks = (int)std::min<long>(1024, (cn + kThreads - 1) / kThreads);
-        hipLaunchKernelGGL(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, width, top[k], left[k],
+        phd_launch(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, width, top[k], left[k],
                            ch, cw, k255, (const double*)nullptr, 0L, sums + 2 * k);
-        hipLaunchKernelGGL(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, width, top[k], left[k],
+        phd_launch(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, width, top[k], left[k],
                            ch, cw, k255, (const double*)(sums + 2 * k), cn, sums + 2 * k + 1);
     }
     return hipGetLastError();

@@ -194,7 +194,7 @@ hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
             hipSuccess || per_cu < 1)
         per_cu = 1;
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
-    hipLaunchKernelGGL(k_rgb_stats, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
+    phd_launch(k_rgb_stats, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
                        a_stride);
     return hipGetLastError();
 }
