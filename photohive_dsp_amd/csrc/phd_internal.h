@@ -224,6 +224,7 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(4000, 3, 256, 5, 8, 10, 10)   \
     X(4000, 4, 384, 5, 8, 10, 10)   \
     X(6000, 0, 512, 6, 10, 10, 10)  \
+    X(6000, 1, 768, 6, 10, 10, 10)  \
     X(3000, 0, 384, 5, 6, 10, 10)   \
     X(2000, 0, 256, 5, 4, 10, 10)
 // columns: X(length, variant, threads per column, flags, radices...); flags:
@@ -231,6 +232,11 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 // Measured at 4000x3000 (tools/ct_sweep.py): v0 54.8 us, v2 55.5, v3 56.0,
 // v4 61.4, v5 61.2, v1 (2 columns, register prefetch, spills) 63.2; global
 // atomic bins 92-148 us (contention), so no variant uses them.
+// Config-5 lengths (tools/ct_sweep.py, 6000x4000 and 4000x6000): columns of
+// 6000 v0 128 us, (10 20 30) 133, 384 threads 143, 768 threads 173; columns
+// of 4000 at 320 threads 126 us, 256 threads 130, (16 25 10) 164, 384
+// threads 182; rows of 6000 at 512 / 768 threads 93 us, 384 threads 103.
+// Columns of 3000 at 320 threads 73 us, 192 threads 67 (v0: 53-58).
 #define PHD_CT_COLS(X)                 \
     X(3000, 0, 256, 5, 15, 10, 20)     \
     X(3000, 1, 384, 2, 5, 6, 10, 10)   \
@@ -239,7 +245,9 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 4, 512, 5, 5, 6, 10, 10)   \
     X(3000, 5, 300, 5, 5, 6, 10, 10)   \
     X(6000, 0, 512, 5, 15, 20, 20)     \
-    X(4000, 0, 256, 5, 10, 20, 20)     \
+    X(6000, 1, 512, 5, 10, 20, 30)     \
+    X(4000, 0, 320, 5, 10, 20, 20)     \
+    X(4000, 1, 256, 5, 10, 20, 20)     \
     X(2000, 0, 256, 5, 10, 10, 20)
 int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
