@@ -61,6 +61,49 @@ def cpu_baseline(h, w, n_images):
                       f"+ scipy.fft.rfft2 (1 worker), {dt:.1f} s"}
 
 
+def single_image(lib, last_error, h=3000, w=4000, iters=20):
+    """BASELINE config 2 as literally stated: ONE 4000x3000 image per call.
+    Median latency of a full report from a device-resident image
+    (phd_report_batch_device, batch 1) and from a host buffer
+    (phd_report_u8: one 36 MB H2D copy included)."""
+    import numpy as np
+    import torch
+    from photohive_dsp_amd.core import make_config
+    from photohive_dsp_amd.structures import Full_Report_Data
+    nb = h * w * 3
+    t = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    assert lib.phd_fill_uniform_device(t.data_ptr(), nb, 77, None) == 0, last_error()
+    host = t.cpu().numpy()
+    cfg = make_config()
+    out = (ctypes.POINTER(Full_Report_Data) * 1)()
+    st = (ctypes.c_int * 1)()
+
+    def dev():
+        if lib.phd_report_batch_device(t.data_ptr(), 1, h, w, nb, ctypes.byref(cfg), out, st, None) != 0:
+            raise RuntimeError(last_error())
+        r = out[0]
+        lib.free_full_report(ctypes.byref(r))
+
+    def hst():
+        r = lib.phd_report_u8(host.ctypes.data, h, w, 0, ctypes.byref(cfg), None)
+        if not r:
+            raise RuntimeError(last_error())
+        lib.free_full_report(ctypes.byref(r))
+
+    res = {}
+    for name, fn in (("device_resident", dev), ("host_buffer", hst)):
+        fn()
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        res[name + "_ms"] = round(1000 * float(np.median(ts)), 3)
+    del t
+    torch.cuda.empty_cache()
+    return {"workload": f"1 x {h}x{w} RGB8 per call, full report, median of {iters}", **res}
+
+
 def config3(lib, last_error, n=512, h=1080, w=1920, iters=10):
     """BASELINE config 3 (the HBM-roofline run): the rgb2hsv + rgb_statistics pass
     (phd_hsv_stats_batch_device, stats.hip) over n device-resident 1080p images, one
@@ -341,6 +384,7 @@ def main():
                             "launches_timed": kern[dom]["launches"], "sampling": "every launch of every 4th step"}
         line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
     if not args.no_config3 and world == 1:
+        line["config2_single"] = single_image(lib, last_error, H, W)
         line["config3"] = config3(lib, last_error)
         line["config4"] = config4(lib, last_error)
         line["config5"] = config5(lib, last_error)
