@@ -320,6 +320,24 @@ def test_runtime_plan_batch_against_oracle(shape):
         assert_report_matches(rep, g)
 
 
+def test_host_batch_rejected_image_keeps_the_others():
+    """phd_report_batch_u8 groups images by size: a rejected size (349x350,
+    pre_compute_error_checks) fails alone, every other image of the batch is
+    reported and matches its single-image report."""
+    phd, L, _ = _phd()
+    from photohive_dsp_amd import synth
+    imgs = [synth.make("structured", 512, 512, 81), np.zeros((349, 350, 3), np.uint8),
+            synth.make("uniform", 480, 640, 82), synth.make("dominant", 512, 512, 83)]
+    reps = phd.get_reports(imgs)
+    assert reps[1] is None
+    for i in (0, 2, 3):
+        one = phd.get_report(imgs[i])
+        assert reps[i].color_palette.group_ids == one.color_palette.group_ids
+        assert reps[i].color_palette.quantities == one.color_palette.quantities
+        np.testing.assert_allclose(np.array(reps[i].blur_profile.bins), np.array(one.blur_profile.bins),
+                                   rtol=1e-12, atol=1e-15)
+
+
 def test_rejections_return_null():
     phd, L, _ = _phd()
     for h, w in [(349, 350), (2001, 400), (400, 2001)]:
