@@ -216,7 +216,11 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 // The first radix is odd (LDS bank-conflict-free first pass, fft_engine.h).
 // Rows need length % 4 == 0.
 // rows: X(length, variant, threads, radices...).  Measured at 4000x3000:
-// v0 43.2 us, v1 43.7, v2 47.3 (25 16 10 at 400 threads), v3 47.3, v4 56.0
+// v0 43.2 us, v1 43.7, v2 47.3 (25 16 10 at 400 threads), v3 47.3, v4 56.0.
+// A last pass that pairs butterflies b and NB - b and separates the two rows'
+// spectra in registers (no LDS write of the last pass, no split reads) was
+// correct (1e-15) but slower: 48.9 us at 256 threads (5 8 10 10), 49.5 at
+// 512 (5 10 20 4, spills), 59.6 / 64.6 at 512 / 384 threads (5 8 10 10).
 #define PHD_CT_ROWS(X)              \
     X(4000, 0, 512, 5, 8, 10, 10)   \
     X(4000, 1, 256, 25, 16, 10)     \
