@@ -8,6 +8,8 @@
 
 #include <thread>
 
+#include <unistd.h>
+
 #include "phd_host.h"
 
 namespace phd {
@@ -277,6 +279,7 @@ void HostPool::worker() {
 }
 
 void HostPool::parallel_for(int n, const std::function<void(int)>& f) {
+    std::lock_guard<std::mutex> job(job_m_);              // one job at a time (contexts of several devices)
     {
         std::lock_guard<std::mutex> lk(m_);
         fn_ = &f;
@@ -293,11 +296,16 @@ void HostPool::parallel_for(int n, const std::function<void(int)>& f) {
 }
 
 HostPool* host_pool() {
-    static HostPool* p = [] {
+    // one pool per process: a forked child has none of its parent's threads
+    static std::mutex m;
+    static HostPool* p = nullptr;
+    static pid_t owner = 0;
+    std::lock_guard<std::mutex> lk(m);
+    if (!p || owner != getpid()) {
         const unsigned hc = std::thread::hardware_concurrency();
-        const int t = hc > 1 ? (int)std::min(hc - 1, 7u) : 0;
-        return new HostPool(t);
-    }();
+        p = new HostPool(hc > 1 ? (int)std::min(hc - 1, 7u) : 0);
+        owner = getpid();
+    }
     return p;
 }
 

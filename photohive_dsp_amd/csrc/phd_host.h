@@ -113,7 +113,7 @@ public:
 private:
     void worker();
     int nthreads_ = 0;
-    std::mutex m_;
+    std::mutex m_, job_m_;
     std::condition_variable cv_, done_;
     const std::function<void(int)>* fn_ = nullptr;
     std::atomic<int> next_{0};
