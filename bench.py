@@ -144,7 +144,7 @@ def config3(lib, last_error, n=512, h=1080, w=1920, iters=10):
                          "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us, 2)}}
 
 
-def config4(lib, last_error, n=32, h=3000, w=4000, iters=3):
+def config4(lib, last_error, n=32, h=3000, w=4000, iters=8):
     """BASELINE config 4 on one GPU: the FFT + blur-profile path alone
     (phd_blur_batch_device) over n device-resident 4000x3000 images.  The
     column pass is this path's dominant kernel: its algorithmic bytes are the
@@ -169,7 +169,7 @@ def config4(lib, last_error, n=32, h=3000, w=4000, iters=3):
             raise RuntimeError(f"blur batch failed: {last_error()}")
     run()
     lib.phd_profile_kernels(0)
-    lib.phd_profile_kernels(0b110)                  # rows and columns
+    lib.phd_profile_kernels(0b110 | (4 << 24))      # rows and columns, every 4th call
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
