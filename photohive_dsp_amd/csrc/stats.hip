@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "phd_device.h"
 
@@ -91,6 +92,7 @@ __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, Sta
 // (or every 1024 items, so the u32 squares cannot overflow: 1024 * 8 groups *
 // 4 * 255^2 < 2^32).  Outputs as K1's statistics-only form: out.sums (6 u64,
 // atomics) and out.s_part[first chunk of the run] (one fp64 per run).
+template <bool kNT>
 __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* const* __restrict__ imgs, long npix,
                                                               int nchunks, long nitems, PaletteDev out,
                                                               long a_stride) {
@@ -115,9 +117,15 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
 #pragma unroll
             for (int st = 0; st < kStGroups; st++) {
                 gu32s* q = (gu32s*)(ip + (off0 + 12u * kStThreads * st));
-                w[st][0] = q[0];
-                w[st][1] = q[1];
-                w[st][2] = q[2];
+                if constexpr (kNT) {                       // streamed once: non-temporal
+                    w[st][0] = __builtin_nontemporal_load(q);
+                    w[st][1] = __builtin_nontemporal_load(q + 1);
+                    w[st][2] = __builtin_nontemporal_load(q + 2);
+                } else {
+                    w[st][0] = q[0];
+                    w[st][1] = q[1];
+                    w[st][2] = q[2];
+                }
             }
 #pragma unroll
             for (int st = 0; st < kStGroups; st++) stat4(w[st][0], w[st][1], w[st][2], a);
@@ -189,13 +197,20 @@ hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
                                   long a_stride, int nchunks, hipStream_t st) {
     const long npix = (long)height * width;
     const long nitems = (long)n * nchunks;
+    // non-temporal loads (the pixels are streamed once): 0.74 of the HBM peak
+    // against 0.70-0.72 with plain loads (PHD_STATS_PLAIN=1)
+    static const bool nt = getenv("PHD_STATS_PLAIN") == nullptr;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_rgb_stats, kStThreads, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_rgb_stats<false>, kStThreads, 0) !=
             hipSuccess || per_cu < 1)
         per_cu = 1;
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
-    phd_launch(k_rgb_stats, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
-                       a_stride);
+    if (nt)
+        phd_launch(k_rgb_stats<true>, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
+                   a_stride);
+    else
+        phd_launch(k_rgb_stats<false>, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
+                   a_stride);
     return hipGetLastError();
 }
 
