@@ -1,15 +1,22 @@
 """Benchmark: images/s of the full PhotoHive_DSP report on 4000x3000 RGB8 images
-(BASELINE.json config 2 at N=1; weak-scaled batches per GPU for N>1).
+(BASELINE.json config 2 at N=1; weak-scaled batches per GPU for N>1), plus the
+other BASELINE configs as objects of the same JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` without a torchrun environment starts the N ranks itself (a
+torchrun child process, before this process touches the GPU) and exits with
+its status.  One process per GPU; rank r uses device r (backend "nccl" = RCCL;
+PHD_BENCH_BACKEND=gloo rehearses N ranks on one GPU).
+
 A step = one full report (stats, S-bar, palette, blur profile, blur vectors)
 of every image of one device-resident batch of B images per GPU.  Images are
 synthetic (splitmix64 uniform RGB8, generated on the device; seed = global
 image index).  Ranks shard images with no data-path collective; one small
-all-reduce merges the counters.  Rank 0 prints one JSON line.
+all-gather merges the counters (shard.merge_counters).  Rank 0 prints one
+JSON line.
 """
 from __future__ import annotations
 
@@ -17,6 +24,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "images/sec (4000×3000 RGB8 full report) at 1/2/4/8 GPUs; HBM GB/s vs peak"
 
 
 def parse(argv=None):
@@ -34,45 +44,247 @@ def parse(argv=None):
     p.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     p.add_argument("--height", type=int, default=3000)
     p.add_argument("--width", type=int, default=4000)
-    p.add_argument("--cpu-images", type=int, default=3, help="CPU baseline sample size (images)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-procs", type=int, default=0,
+                   help="CPU baseline processes (0: the cores this process may use, at most 16)")
     p.add_argument("--no-kernel-events", action="store_true",
                    help="do not bracket kernels with HIP events (roofline then null)")
-    p.add_argument("--no-config3", action="store_true",
-                   help="skip the BASELINE config-3/4 objects (512 x 1080p statistics pass; FFT + blur path)")
+    p.add_argument("--no-configs", "--no-config3", dest="no_configs", action="store_true",
+                   help="headline only: skip the BASELINE config 3/4/5 objects and the host-buffer runs")
+    p.add_argument("--config4-images", type=int, default=2048, help="config 4 total images (all ranks)")
+    p.add_argument("--config5-images", type=int, default=4096, help="config 5 total images (all ranks)")
+    p.add_argument("--plan-only", action="store_true",
+                   help="no GPU: start the ranks, shard configs 2/4/5 and merge the counters (gloo), print the plan")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                    help="per-kernel PMC traffic summary written by tools/pmc_collect.py")
     return p.parse_args(argv)
 
 
-def cpu_baseline(h, w, n_images):
-    """The C restatement of the reference path (oracle/, -O2) + scipy rfft2 (1 worker),
-    one thread, on a bounded sample of the same workload (n_images uniform images)."""
+# ---------------------------------------------------------------------------
+# N ranks from a plain `python bench.py --gpus N`
+# ---------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv=None) -> int:
+    """Start `torch.distributed.run` with N ranks as a CHILD process (nothing in
+    this process has touched the GPU) and return its exit status."""
+    argv = sys.argv[1:] if argv is None else argv
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0 at N=1, before the GPU is touched)
+# ---------------------------------------------------------------------------
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _fft_engine():
+    import ctypes.util
+    fftw = ctypes.util.find_library("fftw3")
+    try:
+        import scipy
+        eng = f"scipy.fft.rfft2 (pocketfft, scipy {scipy.__version__})"
+    except ImportError:
+        eng = "numpy.fft.rfft2"
+    return eng + ("" if fftw is None else f"; libfftw3 present ({fftw}) but not used")
+
+
+def _cpu_worker(job):
+    """One baseline process: the oracle build `opt` on its own images."""
+    opt, h, w, seeds, start_at, fft_workers = job
     from oracle import oracle as orc
     from photohive_dsp_amd import synth
-    imgs = [synth.uniform(h, w, 10_000 + i) for i in range(n_images)]
-    orc.report(synth.uniform(400, 400, 1))        # load the library outside the timing
-    t0 = time.perf_counter()
+    orc.use_build(opt)
+    orc.report(synth.uniform(400, 400, 1))                 # load the library outside the timing
+    imgs = [synth.uniform(h, w, s) for s in seeds]
+    while time.time() < start_at:
+        time.sleep(0.005)
+    t0 = time.time()
     for im in imgs:
-        orc.report(im, fft_workers=1)
-    dt = time.perf_counter() - t0
-    return {"value": n_images / dt, "unit": "images/s", "cores": 1, "kind": "port",
-            "sample": f"{n_images} x {h}x{w} uniform RGB8 full reports, oracle/phd_oracle.c -O2 "
-                      f"+ scipy.fft.rfft2 (1 worker), {dt:.1f} s"}
+        orc.report(im, fft_workers=fft_workers)
+    return len(imgs), t0, time.time()
 
 
-def single_image(lib, last_error, h=3000, w=4000, iters=20):
+def cpu_baseline(h, w, procs):
+    """BASELINE.md 3 / SURVEY.md 8(d): the C restatement of the reference path
+    (oracle/phd_oracle.c + scipy rfft2 for FFTW), u8 host buffer -> full report,
+    on this host's cores.  Throughput mode (the `value`): `procs` independent
+    processes (the reference is not reentrant), one image at a time each, -O2.
+    Latency mode: one image at a time with the FFT on `procs` threads (the
+    reference plans FFTW with num_cores threads), at -O2 and at -O0 (the
+    reference ships -O0)."""
+    import multiprocessing as mp
+    from oracle import oracle as orc
+    from photohive_dsp_amd import synth
+    orc.build()                                            # liboracle.so + liboracle_O0.so (no-op when built)
+    out = {"unit": "images/s", "kind": "port", "cores": procs,
+           "host_cpus_online": os.sysconf("SC_NPROCESSORS_ONLN"), "cpu_model": _cpu_model(),
+           "fft_engine": _fft_engine()}
+    # latency mode: one image at a time, FFT on all `procs` cores
+    lat = {}
+    for opt, n in (("O2", 3), ("O0", 2)):
+        orc.use_build(opt)
+        orc.report(synth.uniform(400, 400, 1))
+        imgs = [synth.uniform(h, w, 20_000 + i) for i in range(n)]
+        t0 = time.perf_counter()
+        for im in imgs:
+            orc.report(im, fft_workers=procs)
+        dt = time.perf_counter() - t0
+        lat[opt] = {"ms_per_image": round(1000 * dt / n, 1), "images_per_s": round(n / dt, 3),
+                    "sample": f"{n} x {h}x{w} uniform, one at a time"}
+    orc.use_build("O2")
+    # throughput mode: `procs` processes, 2 images each, common start
+    per = 2
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        start_at = time.time() + 5.0 + 0.2 * procs
+        jobs = [("O2", h, w, [30_000 + per * p + k for k in range(per)], start_at, 1) for p in range(procs)]
+        res = pool.map(_cpu_worker, jobs, chunksize=1)
+    n_img = sum(r[0] for r in res)
+    wall = max(r[2] for r in res) - min(r[1] for r in res)
+    out["value"] = round(n_img / wall, 3)
+    out["mode"] = "throughput"
+    out["sample"] = (f"{procs} processes x {per} x {h}x{w} uniform RGB8 full reports (-O2 restatement, "
+                     f"1 FFT thread each): {n_img} images in {wall:.1f} s wall")
+    out["modes"] = {"throughput_O2": {"images_per_s": out["value"], "processes": procs},
+                    "latency_O2": lat["O2"], "latency_O0": lat["O0"]}
+    return out
+
+
+# ---------------------------------------------------------------------------
+# GPU configs
+# ---------------------------------------------------------------------------
+def algorithmic_bytes(kernel, h, w):
+    """Bytes one launch must move per image: RGB8 reads of the pixel
+    passes, the fp64-complex half spectrum written by the row pass and read by the
+    column pass, which also reads the u16 polar-bin map (2 B per spectrum element)."""
+    n, hwf = h * w, h * (w // 2 + 1)
+    return {"hsv_stats": 3 * n, "palette_sums": 3 * n, "fft_rows": 3 * n + 16 * hwf,
+            "fft_cols": 18 * hwf, "report": 9 * n + 32 * hwf}.get(kernel)
+
+
+class Ctx:
+    """Per-rank state shared by the configs."""
+
+    def __init__(self, args, world, rank, backend):
+        import torch
+        from photohive_dsp_amd.lib import last_error, lib
+        self.args, self.world, self.rank, self.backend = args, world, rank, backend
+        self.torch, self.lib, self.last_error = torch, lib, last_error
+
+    def barrier(self):
+        if self.world > 1:
+            self.torch.distributed.barrier()
+        self.torch.cuda.synchronize()
+
+    def merge(self, elapsed, images, pixels, alg_bytes, kernel_ms=0.0, launches=0.0):
+        from photohive_dsp_amd.shard import merge_counters
+        return merge_counters([elapsed, images, pixels, alg_bytes, kernel_ms, launches],
+                              device="cuda" if self.backend == "nccl" else "cpu")
+
+    def fill(self, t, seed):
+        assert self.lib.phd_fill_uniform_device(t.data_ptr(), t.numel(), seed, None) == 0, self.last_error()
+
+
+def kernel_times(lib, names):
+    out = {}
+    for k, name in enumerate(names):
+        tot, cnt = ctypes.c_double(), ctypes.c_long()
+        lib.phd_profile_read(k, ctypes.byref(tot), ctypes.byref(cnt))
+        if cnt.value:
+            out[name] = {"total_ms": tot.value, "launches": cnt.value, "avg_us": 1000 * tot.value / cnt.value}
+    return out
+
+
+def headline(cx):
+    """Config 2, weak-scaled: B device-resident 4000x3000 images per rank per step."""
+    args, lib, torch = cx.args, cx.lib, cx.torch
+    from photohive_dsp_amd.core import make_config
+    from photohive_dsp_amd.lib import KERNELS
+    from photohive_dsp_amd.structures import Full_Report_Data
+    H, W, B = args.height, args.width, args.batch
+    img_bytes = H * W * 3
+    d_imgs = torch.empty(B * img_bytes, dtype=torch.uint8, device="cuda")
+    for i in range(B):
+        cx.fill(d_imgs[i * img_bytes:(i + 1) * img_bytes], cx.rank * B + i)
+    torch.cuda.synchronize()
+    cfg = make_config()
+    outs = (ctypes.POINTER(Full_Report_Data) * B)()
+    status = (ctypes.c_int * B)()
+
+    def step():
+        rc = lib.phd_report_batch_device(d_imgs.data_ptr(), B, H, W, img_bytes, ctypes.byref(cfg), outs,
+                                         status, None)
+        if rc != 0:
+            raise RuntimeError(f"report batch failed ({rc}): {cx.last_error()}")
+        for i in range(B):
+            lib.free_full_report(ctypes.byref(outs[i]))
+
+    # warmup; the last warmup step with events on every kernel, to find the
+    # dominant one in steady state
+    lib.phd_profile_kernels(0)
+    for _ in range(max(1, args.warmup) - 1):
+        step()
+    lib.phd_profile_kernels(0 if args.no_kernel_events else (1 << len(KERNELS)) - 1)
+    step()
+    warm = kernel_times(lib, KERNELS)
+    dom = max(warm, key=lambda k: warm[k]["total_ms"]) if warm else None
+    # timed region: HIP events (recorded by the launches themselves, on the
+    # stream the kernel runs on) bracket every launch of the dominant kernel in
+    # every 4th step
+    lib.phd_profile_kernels(0 if dom is None else (1 << KERNELS.index(dom)) | (4 << 24))
+    cx.barrier()
+    t0 = time.perf_counter()
+    stage = [0.0] * 8
+    for _ in range(args.steps):
+        step()
+        tm = (ctypes.c_double * 8)()
+        lib.phd_last_timings(tm, 8)
+        for j in range(8):
+            stage[j] += tm[j]
+    cx.barrier()
+    elapsed = time.perf_counter() - t0
+    kern = kernel_times(lib, KERNELS)
+    lib.phd_profile_kernels(0)
+    n_img = B * args.steps
+    km = kern[dom]["total_ms"] if dom in kern else 0.0
+    kl = kern[dom]["launches"] if dom in kern else 0
+    m = cx.merge(elapsed, n_img, n_img * H * W, n_img * algorithmic_bytes("report", H, W), km, kl)
+    del d_imgs
+    torch.cuda.empty_cache()
+    res = {"merged": m, "dom": dom, "warm": warm, "kern": kern,
+           "stages": {k: stage[j] / args.steps for j, k in enumerate(
+               ("hsv_stats", "fft_rows_cols", "palette_pass2", "gpu_total", "host_total", "host_enqueue",
+                "host_decisions", "host_assembly"))}}
+    return res
+
+
+def single_image(cx, h=3000, w=4000, iters=20):
     """BASELINE config 2 as literally stated: ONE 4000x3000 image per call.
     Median latency of a full report from a device-resident image
     (phd_report_batch_device, batch 1) and from a host buffer
     (phd_report_u8: one 36 MB H2D copy included)."""
     import numpy as np
-    import torch
+    lib, torch = cx.lib, cx.torch
     from photohive_dsp_amd.core import make_config
     from photohive_dsp_amd.structures import Full_Report_Data
     nb = h * w * 3
     t = torch.empty(nb, dtype=torch.uint8, device="cuda")
-    assert lib.phd_fill_uniform_device(t.data_ptr(), nb, 77, None) == 0, last_error()
+    cx.fill(t, 77)
     host = t.cpu().numpy()
     cfg = make_config()
     out = (ctypes.POINTER(Full_Report_Data) * 1)()
@@ -80,14 +292,13 @@ def single_image(lib, last_error, h=3000, w=4000, iters=20):
 
     def dev():
         if lib.phd_report_batch_device(t.data_ptr(), 1, h, w, nb, ctypes.byref(cfg), out, st, None) != 0:
-            raise RuntimeError(last_error())
-        r = out[0]
-        lib.free_full_report(ctypes.byref(r))
+            raise RuntimeError(cx.last_error())
+        lib.free_full_report(ctypes.byref(out[0]))
 
     def hst():
         r = lib.phd_report_u8(host.ctypes.data, h, w, 0, ctypes.byref(cfg), None)
         if not r:
-            raise RuntimeError(last_error())
+            raise RuntimeError(cx.last_error())
         lib.free_full_report(ctypes.byref(r))
 
     res = {}
@@ -104,23 +315,61 @@ def single_image(lib, last_error, h=3000, w=4000, iters=20):
     return {"workload": f"1 x {h}x{w} RGB8 per call, full report, median of {iters}", **res}
 
 
-def config3(lib, last_error, n=512, h=1080, w=1920, iters=10):
+def host_buffers(cx, h=3000, w=4000, n=64, iters=3):
+    """SURVEY.md 8(d)'s end-to-end timed region: u8 HOST buffers in ->
+    Full_Report_Data out, through phd_report_batch_u8 (PCIe H2D included).
+    Pageable numpy buffers, as a Python caller hands them over."""
+    import numpy as np
+    lib, torch = cx.lib, cx.torch
+    from photohive_dsp_amd.core import make_config
+    from photohive_dsp_amd.structures import Full_Report_Data
+    nb = h * w * 3
+    t = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    imgs = []
+    for i in range(n):
+        cx.fill(t, 9000 + i)
+        imgs.append(t.cpu().numpy().copy())
+    del t
+    cfg = make_config()
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in imgs])
+    hs = (ctypes.c_int * n)(*([h] * n))
+    ws = (ctypes.c_int * n)(*([w] * n))
+    outs = (ctypes.POINTER(Full_Report_Data) * n)()
+    st = (ctypes.c_int * n)()
+
+    def run():
+        if lib.phd_report_batch_u8(ptrs, hs, ws, n, ctypes.byref(cfg), outs, st) != 0:
+            raise RuntimeError(cx.last_error())
+        for i in range(n):
+            lib.free_full_report(ctypes.byref(outs[i]))
+    run()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        run()
+    wall = (time.perf_counter() - t0) / iters
+    torch.cuda.empty_cache()
+    return {"workload": f"{n} x {h}x{w} RGB8 pageable host buffers -> reports (phd_report_batch_u8)",
+            "images_per_s": round(n / wall, 1), "h2d_GB_per_s_equiv": round(n * nb / wall / 1e9, 2),
+            "ms_per_batch": round(1000 * wall, 2)}
+
+
+def config3(cx, n=512, h=1080, w=1920, iters=10):
     """BASELINE config 3 (the HBM-roofline run): the rgb2hsv + rgb_statistics pass
     (phd_hsv_stats_batch_device, stats.hip) over n device-resident 1080p images, one
     launch per batch.  Kernel time from HIP events on the launch stream; algorithmic
     bytes = 3 per pixel."""
-    import torch
+    lib, torch = cx.lib, cx.torch
     from photohive_dsp_amd.structures import RGB_Statistics
     nb = h * w * 3
     t = torch.empty(n * nb, dtype=torch.uint8, device="cuda")
     for i in range(n):
-        assert lib.phd_fill_uniform_device(t[i * nb:].data_ptr(), nb, i, None) == 0, last_error()
+        cx.fill(t[i * nb:(i + 1) * nb], i)
     st = (RGB_Statistics * n)()
     sat = (ctypes.c_double * n)()
 
     def run():
         if lib.phd_hsv_stats_batch_device(t.data_ptr(), n, h, w, 0, st, sat, None) != 0:
-            raise RuntimeError(f"hsv_stats batch failed: {last_error()}")
+            raise RuntimeError(f"hsv_stats batch failed: {cx.last_error()}")
     run()
     lib.phd_profile_kernels(0)
     lib.phd_profile_kernels(1)                      # K1 slot = the statistics pass
@@ -144,20 +393,24 @@ def config3(lib, last_error, n=512, h=1080, w=1920, iters=10):
                          "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us, 2)}}
 
 
-def config4(lib, last_error, n=32, h=3000, w=4000, iters=8):
-    """BASELINE config 4 on one GPU: the FFT + blur-profile path alone
-    (phd_blur_batch_device) over n device-resident 4000x3000 images.  The
-    column pass is this path's dominant kernel: its algorithmic bytes are the
-    half spectrum read plus the bin map, 18 * H * (W/2+1) per image (SURVEY.md 8d
-    counts 3N + 32 H Wf = 228 MB for the whole path)."""
+def config4(cx, total, h=3000, w=4000, iters=3):
+    """BASELINE config 4: `total` 4000x3000 images, FFT + blur-profile path alone
+    (phd_blur_batch_device), sharded over the ranks with shard.assign (each rank
+    one call over its device-resident share).  The column pass is this path's
+    dominant kernel: its algorithmic bytes are the half spectrum read plus the
+    bin map, 18 * H * (W/2+1) per image (SURVEY.md 8d counts 3N + 32 H Wf =
+    228 MB for the whole path, the `alg_bytes` counter)."""
     import numpy as np
-    import torch
+    lib, torch = cx.lib, cx.torch
+    from photohive_dsp_amd import shard
     from photohive_dsp_amd.core import make_config
     from photohive_dsp_amd.structures import Blur_Vector
+    mine = shard.assign([(h, w)] * total, cx.world)[cx.rank]
+    n = len(mine)
     nb = h * w * 3
     t = torch.empty(n * nb, dtype=torch.uint8, device="cuda")
-    for i in range(n):
-        assert lib.phd_fill_uniform_device(t[i * nb:].data_ptr(), nb, 1000 + i, None) == 0, last_error()
+    for k, i in enumerate(mine):
+        cx.fill(t[k * nb:(k + 1) * nb], 1000 + i)
     cfg = make_config()
     bins = np.zeros((n, cfg.angle_partitions, cfg.radius_partitions))
     vecs = (Blur_Vector * (10 * n))()
@@ -166,15 +419,16 @@ def config4(lib, last_error, n=32, h=3000, w=4000, iters=8):
     def run():
         if lib.phd_blur_batch_device(t.data_ptr(), n, h, w, 0, ctypes.byref(cfg), bins.ctypes.data_as(P), vecs,
                                      None) != 0:
-            raise RuntimeError(f"blur batch failed: {last_error()}")
+            raise RuntimeError(f"blur batch failed: {cx.last_error()}")
     run()
     lib.phd_profile_kernels(0)
     lib.phd_profile_kernels(0b110 | (4 << 24))      # rows and columns, every 4th call
-    torch.cuda.synchronize()
+    cx.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
         run()
-    wall = (time.perf_counter() - t0) / iters
+    cx.barrier()
+    elapsed = (time.perf_counter() - t0) / iters
     us = {}
     for k, name in ((1, "fft_rows"), (2, "fft_cols")):
         tot, cnt = ctypes.c_double(), ctypes.c_long()
@@ -184,30 +438,37 @@ def config4(lib, last_error, n=32, h=3000, w=4000, iters=8):
     del t
     torch.cuda.empty_cache()
     wf = w // 2 + 1
+    m = cx.merge(elapsed, n, n * h * w, n * (3 * h * w + 32 * h * wf), us["fft_cols"] * n / 1000.0, n)
     ab = 18.0 * h * wf
-    return {"workload": f"{n} x {h}x{w} RGB8, FFT + blur_profile only, device-resident",
-            "images_per_s": round(n / wall, 1), "ms_per_batch_wall": round(1000 * wall, 3),
-            "kernel_us_per_image": {k: round(v, 2) for k, v in us.items()},
+    return {"workload": f"{total} x {h}x{w} RGB8 over {cx.world} GPU, FFT + blur_profile only, device-resident",
+            "scaling": "strong", "n_gpus": cx.world, "images_per_gpu_max": int(np.ceil(total / cx.world)),
+            "images_per_s": round(m["images"] / m["elapsed"], 1),
+            "ms_per_pass_wall": round(1000 * m["elapsed"], 3),
+            "hbm_GB_per_s_path": round(m["alg_bytes"] / m["elapsed"] / 1e9, 1),
+            "kernel_us_per_image_rank0": {k: round(v, 2) for k, v in us.items()},
             "roofline": {"kernel": "fft_cols", "bound": "hbm", "achieved": round(ab / (us["fft_cols"] * 1e-6) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ab / (us["fft_cols"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us["fft_cols"], 2)}}
 
 
-def config5(lib, last_error, n=512, iters=2):
-    """BASELINE config 5 on one GPU: full reports of n device-resident images of
-    mixed sizes (shard.MIXED_SHAPES, 512^2 .. 6000x4000; 512 is one rank's share
-    of the 4096 at 8 GPUs) with h/s/v = 36/4/5, through
-    phd_report_batch_device_mixed (one batched run per size group)."""
-    import torch
+def config5(cx, total, iters=2):
+    """BASELINE config 5: `total` device-resident images of mixed sizes
+    (shard.MIXED_SHAPES, 512^2 .. 6000x4000), full reports at h/s/v = 36/4/5,
+    LPT-sharded by pixel count over the ranks (shard.assign), each rank one
+    phd_report_batch_device_mixed call (one batched run per size group)."""
+    lib, torch = cx.lib, cx.torch
     from photohive_dsp_amd import shard
     from photohive_dsp_amd.core import make_config
     from photohive_dsp_amd.structures import Full_Report_Data
-    sizes = shard.mixed_sizes(n, 5)
+    sizes_all = shard.mixed_sizes(total, 5)
+    mine = shard.assign(sizes_all, cx.world)[cx.rank]
+    sizes = [sizes_all[i] for i in mine]
+    n = len(mine)
     ts = []
-    for i, (h, w) in enumerate(sizes):
+    for i, (h, w) in zip(mine, sizes):
         t = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
-        assert lib.phd_fill_uniform_device(t.data_ptr(), t.numel(), 5000 + i, None) == 0, last_error()
+        cx.fill(t, 5000 + i)
         ts.append(t)
     cfg = make_config(h_partitions=36, s_partitions=4, v_partitions=5)
     ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
@@ -218,43 +479,75 @@ def config5(lib, last_error, n=512, iters=2):
 
     def run():
         if lib.phd_report_batch_device_mixed(ptrs, hs, ws, n, ctypes.byref(cfg), outs, st, None) != 0:
-            raise RuntimeError(f"mixed batch failed: {last_error()}")
+            raise RuntimeError(f"mixed batch failed: {cx.last_error()}")
         for i in range(n):
-            r = outs[i]
-            lib.free_full_report(ctypes.byref(r))
+            lib.free_full_report(ctypes.byref(outs[i]))
     run()
-    torch.cuda.synchronize()
+    cx.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
         run()
-    wall = (time.perf_counter() - t0) / iters
-    mpx = sum(h * w for h, w in sizes) / 1e6
+    cx.barrier()
+    elapsed = (time.perf_counter() - t0) / iters
+    pix = sum(h * w for h, w in sizes)
+    ab = sum(algorithmic_bytes("report", h, w) for h, w in sizes)
+    m = cx.merge(elapsed, n, pix, ab)
     del ts
     torch.cuda.empty_cache()
-    return {"workload": f"{n} mixed-size RGB8 images (seed 5, {len(set(sizes))} sizes, {mpx:.0f} Mpx), "
+    return {"workload": f"{total} mixed-size RGB8 images (seed 5, {len(set(sizes_all))} sizes, "
+                        f"{sum(h * w for h, w in sizes_all) / 1e6:.0f} Mpx) over {cx.world} GPU (LPT by pixels), "
                         "full report, h/s/v 36/4/5, device-resident",
-            "images_per_s": round(n / wall, 1), "megapixels_per_s": round(mpx / wall, 1),
-            "ms_per_batch_wall": round(1000 * wall, 2)}
+            "scaling": "strong", "n_gpus": cx.world,
+            "images_per_s": round(m["images"] / m["elapsed"], 1),
+            "megapixels_per_s": round(m["pixels"] / m["elapsed"] / 1e6, 1),
+            "hbm_GB_per_s_algorithmic": round(m["alg_bytes"] / m["elapsed"] / 1e9, 1),
+            "ms_per_pass_wall": round(1000 * m["elapsed"], 2), "rank_elapsed_ms": [round(1000 * e, 2) for e in m["per_rank_elapsed"]]}
 
 
-def algorithmic_bytes(kernel, h, w):
-    """Bytes one launch must move: RGB8 reads of the pixel passes,
-    the fp64-complex half spectrum written by the row pass and read by the column
-    pass, which also reads the u16 polar-bin map (2 B per spectrum element)."""
-    n, hwf = h * w, h * (w // 2 + 1)
-    return {"hsv_stats": 3 * n, "palette_sums": 3 * n, "fft_rows": 3 * n + 16 * hwf,
-            "fft_cols": 18 * hwf}.get(kernel)
+def plan_only(args, world, rank):
+    """The multi-rank plumbing without a GPU (CPU tests): every rank takes its
+    shard of configs 2, 4 and 5 exactly as the GPU run does and the counters
+    are merged with the same single collective (gloo)."""
+    import torch.distributed as dist
+    from photohive_dsp_amd import shard
+    if world > 1:
+        dist.init_process_group("gloo")
+    H, W, B = args.height, args.width, args.batch
+    c4 = shard.assign([(H, W)] * args.config4_images, world)[rank]
+    sizes5 = shard.mixed_sizes(args.config5_images, 5)
+    c5 = shard.assign(sizes5, world)[rank]
+    out = {}
+    for name, n, pix, ab in (("config2", B, B * H * W, B * algorithmic_bytes("report", H, W)),
+                             ("config4", len(c4), len(c4) * H * W, len(c4) * (3 * H * W + 32 * H * (W // 2 + 1))),
+                             ("config5", len(c5), sum(sizes5[i][0] * sizes5[i][1] for i in c5),
+                              sum(algorithmic_bytes("report", *sizes5[i]) for i in c5))):
+        m = shard.merge_counters([1.0 + rank, n, pix, ab])
+        out[name] = {"images": int(m["images"]), "pixels": int(m["pixels"]), "alg_bytes": int(m["alg_bytes"]),
+                     "elapsed_max": m["elapsed"]}
+    if rank == 0:
+        print(json.dumps({"plan_only": True, "n_gpus": world, **out}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    # PHD_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on one
-    # GPU (RCCL refuses two ranks on one device); the driver's runs use nccl
+    if args.plan_only:
+        return plan_only(args, world, rank)
     backend = os.environ.get("PHD_BENCH_BACKEND", "nccl")
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before this process touches the GPU: the baseline's worker processes
+        # start from a clean parent
+        procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
+        cpu = cpu_baseline(args.height, args.width, procs)
+    import torch
     ndev = torch.cuda.device_count()
     dev = local % ndev if ndev else local
     torch.cuda.set_device(dev)
@@ -265,135 +558,76 @@ def main():
         else:
             dist.init_process_group(backend)
     import photohive_dsp_amd  # noqa: F401
-    from photohive_dsp_amd.core import make_config
-    from photohive_dsp_amd.lib import last_error, lib
-    from photohive_dsp_amd.structures import Full_Report_Data
+    cx = Ctx(args, world, rank, backend)
 
-    H, W, B = args.height, args.width, args.batch
-    img_bytes = H * W * 3
-    d_imgs = torch.empty(B * img_bytes, dtype=torch.uint8, device="cuda")
-    for i in range(B):
-        seed = rank * B + i
-        sub = d_imgs[i * img_bytes:(i + 1) * img_bytes]
-        assert lib.phd_fill_uniform_device(sub.data_ptr(), img_bytes, seed, None) == 0, last_error()
-    torch.cuda.synchronize()
-    cfg = make_config()
-    outs = (ctypes.POINTER(Full_Report_Data) * B)()
-    status = (ctypes.c_int * B)()
-
-    def step():
-        rc = lib.phd_report_batch_device(d_imgs.data_ptr(), B, H, W, img_bytes, ctypes.byref(cfg), outs,
-                                         status, None)
-        if rc != 0:
-            raise RuntimeError(f"report batch failed ({rc}): {last_error()}")
-        for i in range(B):
-            lib.free_full_report(ctypes.byref(outs[i]))
-
-    from photohive_dsp_amd.lib import KERNELS
-
-    def kernel_times():
-        out = {}
-        for k, name in enumerate(KERNELS):
-            tot, cnt = ctypes.c_double(), ctypes.c_long()
-            lib.phd_profile_read(k, ctypes.byref(tot), ctypes.byref(cnt))
-            if cnt.value:
-                out[name] = {"total_ms": tot.value, "launches": cnt.value, "avg_us": 1000 * tot.value / cnt.value}
-        return out
-
-    # warmup; the last warmup step with events on every kernel, to find the
-    # dominant one in steady state
-    lib.phd_profile_kernels(0)
-    for _ in range(max(1, args.warmup) - 1):
-        step()
-    lib.phd_profile_kernels(0 if args.no_kernel_events else (1 << len(KERNELS)) - 1)
-    step()
-    warm = kernel_times()
-    dom = max(warm, key=lambda k: warm[k]["total_ms"]) if warm else None
-
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-
-    # timed region: HIP events bracket every launch of the dominant kernel in
-    # every 4th step (bracketing every launch of every step costs ~6% throughput)
-    lib.phd_profile_kernels(0 if dom is None else (1 << KERNELS.index(dom)) | (4 << 24))
-    barrier()
-    t0 = time.perf_counter()
-    stage = [0.0] * 8
-    for _ in range(args.steps):
-        step()
-        tm = (ctypes.c_double * 8)()
-        lib.phd_last_timings(tm, 8)
-        for j in range(8):
-            stage[j] += tm[j]
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kern = kernel_times()
-
-    # the single collective: max of wall time, sums of images / pixels (shard.py)
-    from photohive_dsp_amd.shard import merge_counters
-    elapsed, images, _ = merge_counters(elapsed, float(B * args.steps), float(B * args.steps * H * W),
-                                        device="cuda" if backend == "nccl" else "cpu")
-    if rank != 0:
-        if world > 1:
-            torch.distributed.destroy_process_group()
-        return
-    value = images / elapsed
-    line = {
-        "metric": "images/sec (4000\u00d73000 RGB8 full report) at 1/2/4/8 GPUs; HBM GB/s vs peak",
-        "value": round(value, 3),
-        "unit": "images/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1000 * elapsed / args.steps, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (device splitmix64 uniform RGB8)",
-        "config": {"workload": f"full report, {H}x{W} RGB8, batch {B}/GPU, device-resident",
-                   "global_batch": B * world, "image": f"{H}x{W}", "parallelism": f"images sharded over {world} GPU"},
-        "stages_ms_per_step": {"hsv_stats": stage[0] / args.steps, "fft_rows_cols": stage[1] / args.steps,
-                               "palette_pass2": stage[2] / args.steps, "gpu_total": stage[3] / args.steps,
-                               "host_total": stage[4] / args.steps, "host_enqueue": stage[5] / args.steps,
-                               "host_decisions": stage[6] / args.steps, "host_assembly": stage[7] / args.steps},
-    }
-    line["roofline"] = None
-    if dom in kern:
-        # the palette passes take the whole batch in one launch, the FFT passes one image
-        # (from the last warmup step, whose every launch was bracketed)
-        per_launch = B / warm[dom]["launches"]
-        ab = algorithmic_bytes(dom, H, W) * per_launch
-        achieved = ab / (kern[dom]["avg_us"] * 1e-6) / 1e9
-        traffic = None
-        try:
-            with open(args.pmc) as f:
-                pm = json.load(f)
-            if pm.get("image") == f"{H}x{W}" and dom in pm.get("kernels", {}):
-                traffic = pm["kernels"][dom]["hbm_bytes_per_image"] * per_launch
-        except (OSError, ValueError, KeyError):
-            pass
-        line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                            "traffic": traffic, "algorithmic_bytes_per_launch": ab,
-                            "images_per_launch": per_launch,
-                            "avg_launch_us": round(kern[dom]["avg_us"], 2),
-                            "launches_timed": kern[dom]["launches"], "sampling": "every launch of every 4th step"}
-        line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
-    if not args.no_config3 and world == 1:
-        line["config2_single"] = single_image(lib, last_error, H, W)
-        line["config3"] = config3(lib, last_error)
-        line["config4"] = config4(lib, last_error)
-        line["config5"] = config5(lib, last_error)
-    if not args.no_cpu_baseline and world == 1:     # rank 0 at N=1 only
-        line["cpu_baseline"] = cpu_baseline(H, W, args.cpu_images)
-    print(json.dumps(line), flush=True)
+    hl = headline(cx)
+    extra = {}
+    if not args.no_configs:
+        extra["config4"] = config4(cx, args.config4_images)
+        extra["config5"] = config5(cx, args.config5_images)
+        if world == 1:
+            extra["config2_single"] = single_image(cx, args.height, args.width)
+            extra["host_buffer"] = host_buffers(cx, args.height, args.width)
+            extra["config3"] = config3(cx)
+    if rank == 0:
+        m = hl["merged"]
+        H, W, B = args.height, args.width, args.batch
+        value = m["images"] / m["elapsed"]
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * m["elapsed"] / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (device splitmix64 uniform RGB8)",
+            "config": {"workload": f"full report, {H}x{W} RGB8, batch {B}/GPU, device-resident",
+                       "global_batch": B * world, "image": f"{H}x{W}",
+                       "parallelism": f"images sharded over {world} GPU"},
+            "hbm_GB_per_s_algorithmic": round(m["alg_bytes"] / m["elapsed"] / 1e9, 1),
+            "stages_ms_per_step_rank0": hl["stages"],
+        }
+        dom, warm, kern = hl["dom"], hl["warm"], hl["kern"]
+        line["roofline"] = None
+        if dom in kern:
+            # the palette passes take the whole batch in one launch, the FFT passes one image
+            # (from the last warmup step, whose every launch was bracketed)
+            per_launch = B / warm[dom]["launches"]
+            ab = algorithmic_bytes(dom, H, W) * per_launch
+            # every rank's sampled launches of the dominant kernel (counter all-gather)
+            avg_us = 1000 * m["kernel_ms"] / max(m["launches"], 1)
+            achieved = ab / (avg_us * 1e-6) / 1e9
+            traffic, tsrc = None, None
+            try:
+                with open(args.pmc) as f:
+                    pm = json.load(f)
+                if pm.get("image") == f"{H}x{W}" and dom in pm.get("kernels", {}):
+                    traffic = pm["kernels"][dom]["hbm_bytes_per_image"] * per_launch
+                    tsrc = (f"{os.path.relpath(args.pmc, ROOT)}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                            "passes of this config (tools/pmc_collect.py), not measured in this run")
+            except (OSError, ValueError, KeyError):
+                pass
+            line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": ab,
+                                "images_per_launch": per_launch, "avg_launch_us": round(avg_us, 2),
+                                "launches_timed": int(m["launches"]),
+                                "sampling": "every launch of every 4th timed step, all ranks"}
+            line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
+        line.update(extra)
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
+            line["vs_cpu_baseline"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

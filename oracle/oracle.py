@@ -47,6 +47,15 @@ def build() -> None:
 _lib = None
 
 
+def use_build(opt: str = "O2") -> None:
+    """Select the restatement's build: "O2" (liboracle.so) or "O0"
+    (liboracle_O0.so, the optimisation level the reference ships at).
+    Only bench.py's cpu_baseline leg switches builds."""
+    global SO, _lib
+    SO = os.path.join(HERE, "liboracle.so" if opt == "O2" else f"liboracle_{opt}.so")
+    _lib = None
+
+
 def lib():
     global _lib
     if _lib is None:

@@ -27,6 +27,15 @@ DEFAULTS = dict(h_partitions=18, s_partitions=2, v_partitions=3, black_thresh=0.
                 fft_streak_thresh=1.20, magnitude_thresh=0.3, blur_cutoff_ratio_denom=2)
 
 
+def _stream_handle(stream):
+    """The hipStream_t a device call runs on: the given torch stream, else
+    torch's current stream (its handle 0, the null stream, makes the library
+    order its own stream after the null stream's prior work)."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream or None
+
+
 def make_config(**kw) -> PhdConfig:
     c = dict(DEFAULTS)
     unknown = set(kw) - set(c)
@@ -207,7 +216,7 @@ def report_device(images, stream=None, **kw):
     cfg = make_config(**kw)
     outs = (POINTER(Full_Report_Data) * n)()
     st = (ctypes.c_int * n)()
-    s = stream.cuda_stream if stream is not None else None
+    s = _stream_handle(stream)
     lib.phd_report_batch_device(images.data_ptr(), n, h, w, 0, ctypes.byref(cfg), outs, st, s)
     res = [(_finish(outs[i], h, w, kw) if st[i] == 0 else None) for i in range(n)]
     if any(r is None for r in res):
@@ -229,7 +238,7 @@ def reports_device_mixed(images, stream=None, **kw):
     ws = (ctypes.c_int * n)(*[int(im.shape[1]) for im in images])
     outs = (POINTER(Full_Report_Data) * n)()
     st = (ctypes.c_int * n)()
-    s = stream.cuda_stream if stream is not None else None
+    s = _stream_handle(stream)
     lib.phd_report_batch_device_mixed(ptrs, hs, ws, n, ctypes.byref(cfg), outs, st, s)
     res = [(_finish(outs[i], hs[i], ws[i], kw) if st[i] == 0 else None) for i in range(n)]
     if any(r is None for r in res):
@@ -246,7 +255,7 @@ def hsv_stats_device(images, stream=None):
     n, h, w = int(images.shape[0]), int(images.shape[1]), int(images.shape[2])
     stats = (RGB_Statistics * n)()
     sat = (ctypes.c_double * n)()
-    s = stream.cuda_stream if stream is not None else None
+    s = _stream_handle(stream)
     if lib.phd_hsv_stats_batch_device(images.data_ptr(), n, h, w, 0, stats, sat, s) != 0:
         raise RuntimeError(f"hsv_stats_device failed: {last_error()}")
     return list(stats), list(sat)
@@ -265,7 +274,7 @@ def blur_profiles_device(images, stream=None, **kw):
     na, nr = cfg.angle_partitions, cfg.radius_partitions
     bins = np.zeros((n, na, nr), dtype=np.float64)
     vecs = (Blur_Vector * (10 * n))()
-    s = stream.cuda_stream if stream is not None else None
+    s = _stream_handle(stream)
     if lib.phd_blur_batch_device(images.data_ptr(), n, h, w, 0, ctypes.byref(cfg),
                                  bins.ctypes.data_as(POINTER(ctypes.c_double)), vecs, s) != 0:
         raise RuntimeError(f"blur_profiles_device failed: {last_error()}")

@@ -295,24 +295,24 @@ __global__ __launch_bounds__(T) void k_fft_rows(const uint8_t* __restrict__ img0
 template <int T, bool GEN>
 __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inter0, size_t inter_stride, int H,
                                                 int wf, int C, FftPlan plan, const uint16_t* __restrict__ binmap,
-                                                int nbins, int lds_bins, double* __restrict__ bin_sums0,
+                                                int nbins, int lds_bins, unsigned long long* __restrict__ bin_sums0,
                                                 double* __restrict__ fmax_part0, long out_stride, int ablate) {
     // blockIdx.y: the image of a batch (inter0 + y * inter_stride elements,
     // bin sums and max partials at + y * out_stride doubles)
     const double2* inter = inter0 + (size_t)blockIdx.y * inter_stride;
-    double* bin_sums = bin_sums0 + (size_t)blockIdx.y * out_stride;
+    unsigned long long* bin_sums = bin_sums0 + (size_t)blockIdx.y * out_stride;
     double* fmax_part = fmax_part0 + (size_t)blockIdx.y * out_stride;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
     double2* tw = buf + (size_t)C * H;
-    double* lb = reinterpret_cast<double*>(tw + 64 + plan.n_hi);
+    unsigned long long* lb = reinterpret_cast<unsigned long long*>(tw + 64 + plan.n_hi);
     const int tid = threadIdx.x;
     const int cb = blockIdx.x;
     const int k0 = cb * C;
     const int nc = min(C, wf - k0);
     load_twiddles(tw, plan);
     if (lds_bins)
-        for (int i = tid; i < nbins; i += T) lb[i] = 0.0;
+        for (int i = tid; i < nbins; i += T) lb[i] = 0ull;
     {
         // the nc columns are one contiguous run of the column-major spectrum
         const double2* src = inter + (size_t)k0 * H;
@@ -321,12 +321,12 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
     __syncthreads();
     if (!(ablate & 1)) fft_lds<T, GEN>(buf, nc, plan, tw, tw + 64);
     double mx = 0.0;
-    double* acc = lds_bins ? lb : bin_sums;
+    unsigned long long* acc = lds_bins ? lb : bin_sums;
     const int total = (ablate & 2) ? 0 : nc * H;
     for (int i0 = 0; i0 < total; i0 += T) {
         const int i = i0 + tid;
         int b = -1;
-        double lg = 0.0;
+        unsigned long long lg = 0ull;
         if (i < total) {
             const double2 X = buf[i];
             const double p = X.x * X.x + X.y * X.y;      // fft_processing.c:49
@@ -334,12 +334,13 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
             if (p >= 1) {                               // fft_processing.c:197-198
                 const int c = i / H, u = i - c * H;
                 b = binmap[(size_t)(k0 + c) * H + u];
-                lg = log(p);
+                lg = bin_fixed(log(p));
             }
         }
+        // fixed-point integers: the sums do not depend on the atomics' order
         const int b0 = __builtin_amdgcn_readfirstlane(b);
         if (__all(b == b0)) {
-            const double t = wave_sum(lg);
+            const unsigned long long t = wave_sum(lg);
             if (b0 >= 0 && lane_id() == 0) atomicAdd(&acc[b0], t);
         } else if (b >= 0) {
             atomicAdd(&acc[b], lg);
@@ -359,8 +360,8 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
     }
     if (lds_bins && !(ablate & 4)) {
         for (int i = tid; i < nbins; i += T) {
-            const double a = lb[i];
-            if (a != 0.0) atomicAdd(&bin_sums[i], a);
+            const unsigned long long a = lb[i];
+            if (a != 0ull) atomicAdd(&bin_sums[i], a);
         }
     }
 }
@@ -414,7 +415,7 @@ hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftP
 template <int T, bool GEN>
 static hipError_t cols_impl(const double2* inter, size_t inter_stride, int n, int height, int wf, int C,
                             const FftPlan& plan, const uint16_t* binmap, int nbins, int lds_bins, size_t lds,
-                            double* bin_sums, double* fmax_part, long out_stride, hipStream_t st) {
+                            unsigned long long* bin_sums, double* fmax_part, long out_stride, hipStream_t st) {
     static bool once = (allow_big_lds(k_fft_cols<T, GEN>), true);
     (void)once;
     static const int ablate = getenv("PHD_ABLATE") ? atoi(getenv("PHD_ABLATE")) : 0;   // debug only
@@ -425,7 +426,7 @@ static hipError_t cols_impl(const double2* inter, size_t inter_stride, int n, in
 
 int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds_out, int* lds_bins_out) {
     constexpr size_t kLdsBudget = 158 * 1024;
-    const size_t bins_bytes = sizeof(double) * nbins;
+    const size_t bins_bytes = sizeof(unsigned long long) * nbins;
     const int lds_bins = bins_bytes <= 48 * 1024;
     const size_t fixed = sizeof(double2) * (64 + plan.n_hi) + (lds_bins ? bins_bytes : 0);
     const size_t col_bytes = sizeof(double2) * height;
@@ -439,7 +440,7 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 
 template <bool GEN>
 static hipError_t cols_t(const double2* inter0, size_t inter_stride, int n, int height, int wf, const FftPlan& plan,
-                         const uint16_t* binmap, int nbins, double* bin_sums0, double* fmax_part0, long out_stride,
+                         const uint16_t* binmap, int nbins, unsigned long long* bin_sums0, double* fmax_part0, long out_stride,
                          hipStream_t st) {
     size_t lds;
     int lds_bins;
@@ -452,7 +453,7 @@ static hipError_t cols_t(const double2* inter0, size_t inter_stride, int n, int 
 }
 
 hipError_t launch_fft_cols_batch(const double2* inter0, size_t inter_stride, int n, int height, int wf,
-                                 const FftPlan& plan, const uint16_t* binmap, int nbins, double* bin_sums0,
+                                 const FftPlan& plan, const uint16_t* binmap, int nbins, unsigned long long* bin_sums0,
                                  double* fmax_part0, long out_stride, hipStream_t st) {
     return plan.generic ? cols_t<true>(inter0, inter_stride, n, height, wf, plan, binmap, nbins, bin_sums0,
                                        fmax_part0, out_stride, st)
@@ -461,7 +462,7 @@ hipError_t launch_fft_cols_batch(const double2* inter0, size_t inter_stride, int
 }
 
 hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
-                           const uint16_t* binmap, int nbins, double* bin_sums,
+                           const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
                            double* fmax_part, hipStream_t st) {
     return launch_fft_cols_batch(inter, 0, 1, height, wf, plan, binmap, nbins, bin_sums, fmax_part, 0, st);
 }

@@ -242,7 +242,7 @@ struct ColK {
     static constexpr int NT = NC * T;                                     // block size
     static constexpr int CR = (2 * NC * P + NT - 1) / NT;                 // load rounds
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
-    static size_t lds(int nbins) { return sizeof(double2) * (NC * H + NTW) + (GB ? 0 : sizeof(double) * nbins); }
+    static size_t lds(int nbins) { return sizeof(double2) * (NC * H + NTW) + (GB ? 0 : sizeof(unsigned long long) * nbins); }
     static_assert(Radices<Rs...>::product == H, "plan");
     // waves per SIMD of the launch bounds: one-column blocks are sized for two
     // resident blocks per CU, one when the column and twiddles fill the LDS
@@ -260,7 +260,7 @@ struct ColK {
 template <int H, int T, int CPB, int... Rs>
 __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter, int wf,
                                                      const uint16_t* __restrict__ binmap, int nbins,
-                                                     double* __restrict__ bin_sums, double* __restrict__ fmax_part,
+                                                     unsigned long long* __restrict__ bin_sums, double* __restrict__ fmax_part,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums, int width,
                                                      double* __restrict__ dbg, int ablate_arg) {
@@ -272,7 +272,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* bufs = reinterpret_cast<double2*>(smem);         // [CPB][H]
     double2* tw = bufs + NC * H;
-    double* lb = reinterpret_cast<double*>(tw + K::NTW);
+    unsigned long long* lb = reinterpret_cast<unsigned long long*>(tw + K::NTW);
     const int tid = threadIdx.x;
     // NC == 1: blocks b, b^8, b^16, b^24 (one XCD) take the four columns of a
     // 128-byte line (two tiles), so each line is fetched once into that L2
@@ -282,8 +282,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     double2* buf = bufs + (NC == 2 ? half * H : 0);
     for (int i = tid; i < K::NTW; i += NT) tw[i] = twg[i];
     if (!K::GB)
-        for (int i = tid; i < nbins; i += NT) lb[i] = 0.0;
-    double* const bsum = K::GB ? bin_sums : lb;          // where the runs are added
+        for (int i = tid; i < nbins; i += NT) lb[i] = 0ull;
+    unsigned long long* const bsum = K::GB ? bin_sums : lb;   // where the runs are added
     const int kpn = (wf + 1) / 2;
     const int nunit = NC == 2 ? kpn : (kpn + 1) / 2;          // column pairs / tile pairs
     const int nlog = NC == 2 ? (int)gridDim.x : (int)gridDim.x / 4;
@@ -384,7 +384,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         }
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
-        // few tens of rows along a column)
+        // few tens of rows along a column), in kBinScale fixed point so that the
+        // sums do not depend on the order of the atomics
         if (!(ablate & 2)) {
             int cur = -1;
             double acc = 0.0;
@@ -396,7 +397,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     if (lg >= 0.0) {
                         const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
                         if (bin != cur) {
-                            if (cur >= 0) atomicAdd(&bsum[cur], acc);
+                            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc));
                             cur = bin;
                             acc = 0.0;
                         }
@@ -404,7 +405,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     }
                 }
             }
-            if (cur >= 0) atomicAdd(&bsum[cur], acc);
+            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc));
         }
         __syncthreads();
     }
@@ -420,8 +421,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         fmax_part[blockIdx.x] = m;
     }
     for (int i = tid; i < nbins && !K::GB && !(ablate & 8); i += NT) {
-        const double t = lb[i];
-        if (t != 0.0) atomicAdd(&bin_sums[i], t);
+        const unsigned long long t = lb[i];
+        if (t != 0ull) atomicAdd(&bin_sums[i], t);
     }
 }
 
@@ -463,7 +464,7 @@ int cols_grid(int wf, int nbins) {
 }
 
 template <int H, int T, int CPB, int... Rs>
-hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binmap, int nbins, double* bin_sums,
+hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st) {
     const size_t lds = ColK<H, T, CPB, Rs...>::lds(nbins);
@@ -550,7 +551,7 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 }
 
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,
-                              int nbins, double* bin_sums, double* fmax_part, const double2* tw,
+                              int nbins, unsigned long long* bin_sums, double* fmax_part, const double2* tw,
                               const unsigned long long* sums, double* dbg, hipStream_t st) {
     const int n_ = height;
 #define PHD_X(N, V, T, ...) \

@@ -24,7 +24,10 @@ Context* g_ctx[64] = {};
 
 void set_error(const std::string& msg) {
     g_error = msg;
-    if (!getenv("PHD_QUIET")) fprintf(stderr, "photohive_dsp_amd: %s\n", msg.c_str());
+    // the reference's own messages (pre_compute_error_checks, src/utilities.c:64-87)
+    // are printed verbatim; the library's own ones carry the same "Error: " prefix
+    if (!getenv("PHD_QUIET"))
+        fprintf(stderr, "%s%s\n", msg.compare(0, 7, "Error: ") == 0 ? "" : "Error: ", msg.c_str());
 }
 void clear_error() { g_error.clear(); }
 
@@ -76,13 +79,22 @@ Context* get_context() {
         hipEventCreateWithFlags(&c->ev_rows[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_rows[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_cols[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_cols[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_cols[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_null, hipEventDisableTiming) != hipSuccess) {
         set_error("hipStreamCreate failed");
         delete c;
         return nullptr;
     }
     g_ctx[dev] = c;
     return c;
+}
+
+hipStream_t work_stream(Context* c, void* stream) {
+    if (stream) return (hipStream_t)stream;
+    // the library stream is non-blocking: without this it would not wait for
+    // work the caller queued on the null stream (e.g. a torch op producing the input)
+    if (hipEventRecord(c->ev_null, nullptr) == hipSuccess) (void)hipStreamWaitEvent(c->stream, c->ev_null, 0);
+    return c->stream;
 }
 
 bool ensure_device(void** p, size_t* cap, size_t need) {
@@ -238,7 +250,7 @@ hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int 
 }
 
 hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int width, int wf,
-                           const uint16_t* binmap, int nbins, double* bin_sums, double* fmax_part,
+                           const uint16_t* binmap, int nbins, unsigned long long* bin_sums, double* fmax_part,
                            const unsigned long long* sums, double* dbg, hipStream_t st) {
     if (s.ct)
         return launch_fft_cols_ct(inter, height, width, wf, binmap, nbins, bin_sums, fmax_part, s.tw_c, sums, dbg,

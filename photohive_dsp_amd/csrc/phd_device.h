@@ -316,6 +316,9 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// a non-negative sum of log(p) as kBinScale fixed point (round to nearest)
+__device__ __forceinline__ unsigned long long bin_fixed(double x) { return __double2ull_rn(x * kBinScale); }
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));

@@ -166,10 +166,16 @@ struct Context {
     hipStream_t dl = nullptr;
     std::vector<hipEvent_t> ev_img_fft, ev_img_dl;
     KernelProfiler prof;
+    hipEvent_t ev_null = nullptr;                   // orders the library stream after the null stream
     std::mutex mu;
 };
 // The context of the current HIP device (created on first use).  nullptr if no GPU.
 Context* get_context();
+// The stream a call works on: the caller's, or (NULL) the library's own stream
+// ordered after every prior operation of the legacy null stream, so device
+// buffers a caller (or PyTorch's default stream) is still producing are
+// complete before the library reads them.
+hipStream_t work_stream(Context* c, void* stream);
 bool ensure_device(void** p, size_t* cap, size_t need);
 bool ensure_pinned(Context* c, size_t need);
 const FftPlanHost* get_plan(Context* c, int n);
@@ -192,7 +198,7 @@ hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int 
                            unsigned long long* rsum = nullptr);
 // sums: K1's channel sums of the image (the compile-time column pass removes the DC bias)
 hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int width, int wf,
-                           const uint16_t* binmap, int nbins, double* bin_sums, double* fmax_part,
+                           const uint16_t* binmap, int nbins, unsigned long long* bin_sums, double* fmax_part,
                            const unsigned long long* sums, double* dbg, hipStream_t st);
 const BlurTable* get_table(Context* c, int height, int width, int nr, int na);
 // Classification tables of a grid (uploaded once per configuration).

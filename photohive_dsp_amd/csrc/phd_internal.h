@@ -29,6 +29,14 @@ constexpr int kThreads = 256;
 // Largest FFT length kept resident in LDS (complex fp64, 16 B/element).
 constexpr int kFftMaxLds = 8192;
 constexpr int kMaxFftPasses = 24;
+// Polar-bin sums of log(p) are accumulated as unsigned 64-bit fixed point
+// (value * 2^32): integer additions commute, so the bins -- and the strict
+// threshold comparisons vectorize_blur_profile makes on them -- are the same
+// on every run whatever order the atomics land in.  A bin's sum stays below
+// 60M elements x log(1.5e16) = 2.2e9 < 2^31 for any image the reference
+// accepts (120 MP), so it fits; one run's rounding is <= 2^-33.
+constexpr double kBinScale = 4294967296.0;
+constexpr double kBinInvScale = 1.0 / 4294967296.0;
 
 // The HSV grid of initialize_octree (src/color_quantization.c:22-101).
 struct GridParams {
@@ -196,16 +204,16 @@ hipError_t launch_fft_rows_batch(const uint8_t* const* d_imgs, int n, int height
                                  const unsigned long long* sums0, long sums_stride, const double* k255,
                                  double2* inter0, size_t inter_stride, hipStream_t st);
 hipError_t launch_fft_cols_batch(const double2* inter0, size_t inter_stride, int n, int height, int wf,
-                                 const FftPlan& plan, const uint16_t* binmap, int nbins, double* bin_sums0,
+                                 const FftPlan& plan, const uint16_t* binmap, int nbins, unsigned long long* bin_sums0,
                                  double* fmax_part0, long out_stride, hipStream_t st);
 hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftPlan& plan,
                            const unsigned long long* sums, const double* k255,
                            double2* inter, hipStream_t st);
 // Column pass + epilogue: power, running max, sum log(p) over p >= 1 per
 // polar bin (binmap[wf][height], uint16 bin ids).  Accumulates into
-// bin_sums[na*nr] (fp64) and writes one max power per block to fmax_part.
+// bin_sums[na*nr] (kBinScale fixed point) and writes one max power per block to fmax_part.
 hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
-                           const uint16_t* binmap, int nbins, double* bin_sums,
+                           const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
                            double* fmax_part, hipStream_t st);
 // Column blocks of launch_fft_cols (= entries of fmax_part); optional LDS size.
 int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds, int* lds_bins);
@@ -268,7 +276,7 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 // The column pass removes the DC bias (K1's channel sums) from column 0 first.
 // dbg (optional): the power spectrum, column-major [wf][height]
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,
-                              int nbins, double* bin_sums, double* fmax_part, const double2* tw,
+                              int nbins, unsigned long long* bin_sums, double* fmax_part, const double2* tw,
                               const unsigned long long* sums, double* dbg, hipStream_t st);
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st);

@@ -99,17 +99,17 @@ bool check_crops(const Crop_Boundaries* cb, int height, int width) {
 // pre_compute_error_checks (src/utilities.c:64-87) on the dimensions.
 bool precheck(int height, int width) {
     if (height < 350 || width < 350) {
-        set_error("Image height and width must be greater than 350. Height: " + std::to_string(height) +
+        set_error("Error: Image height and width must be greater than 350. Height: " + std::to_string(height) +
                   "\tWidth" + std::to_string(width));
         return false;
     }
     if ((long long)height * width > 120000000LL) {
-        set_error("Image must have less than 120000000 pixels.");
+        set_error("Error: Image must have less than 120000000 pixels.");
         return false;
     }
     const float ar = (float)height / (float)width;
     if (ar < 1.0 / 5.0 || ar > 5.0 / 1.0) {
-        set_error("Invalid aspect ratio: " + std::to_string(ar));
+        set_error("Error: Invalid aspect ratio: " + std::to_string(ar));
         return false;
     }
     return true;
@@ -129,20 +129,21 @@ float ms_between(hipEvent_t a, hipEvent_t b) {
 // pgm_normalize_fft's G_s (src/fft_processing.c:192) applied to the binned
 // sums of log(p); calculate_blur_profile's averaging (src/blur_profile.c:106-116);
 // vectorize_blur_profile (src/blur_profile.c:324-416).  flat: na x nr.
-void finish_blur(const BlurTable& tbl, const double* bin_sums, double fmax, const phd_config& cfg, double* flat,
-                 Blur_Vector* vectors) {
+void finish_blur(const BlurTable& tbl, const unsigned long long* bin_sums, double fmax, const phd_config& cfg,
+                 double* flat, Blur_Vector* vectors) {
     const int na = cfg.angle_partitions, nr = cfg.radius_partitions;
     const double gs = 1 / (2 * std::log(std::sqrt(fmax) + 1));
     for (size_t b = 0; b < (size_t)na * nr; b++) {
         const double q = (double)tbl.counts[b];
-        const double sum = bin_sums[b] == 0.0 ? 0.0 : bin_sums[b] * gs;
+        // the device sums are kBinScale fixed point (order-independent)
+        const double sum = bin_sums[b] == 0ull ? 0.0 : (double)bin_sums[b] * kBinInvScale * gs;
         flat[b] = q != 0 ? sum / q : 0;
     }
     vectorize_blur(flat, na, nr, cfg.fft_streak_thresh, cfg.magnitude_thresh, cfg.blur_cutoff_ratio_denom, vectors);
 }
 
 Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const PaletteDecision& dec,
-                           const double* pal, long n_hsv, const BlurTable& tbl, const double* bin_sums,
+                           const double* pal, long n_hsv, const BlurTable& tbl, const unsigned long long* bin_sums,
                            double fmax, const phd_config& cfg, const Crop_Boundaries* crops,
                            const double* sharp_sums, std::string* why) {
     const int np = (int)dec.parents.size();
@@ -253,10 +254,12 @@ bool launch_k1(Context* c, const Layout& L, int n, const uint8_t* const* d_imgs,
     pd.chunk_hist = (unsigned short*)(dw + L.H(n, 0));
     pd.gsum = (double*)(dw + L.A(0) + L.a_gsum);
     pd.gcell = (unsigned*)(dw + L.A(0) + L.a_gcell);
+    // the device image-pointer array: K1 (ds == 1), the batched runtime-plan FFT
+    // passes and the batched palette tail read it, whatever the downsample rate
+    memcpy(hp + L.P_pin(n), d_imgs, sizeof(void*) * n);
+    PHD_HIP(hipMemcpyAsync(dw + L.P_dev(n), hp + L.P_pin(n), sizeof(void*) * n, hipMemcpyHostToDevice, st));
     const int ps = c->prof.begin(kK1, st);
     if (ds <= 1) {
-        memcpy(hp + L.P_pin(n), d_imgs, sizeof(void*) * n);
-        PHD_HIP(hipMemcpyAsync(dw + L.P_dev(n), hp + L.P_pin(n), sizeof(void*) * n, hipMemcpyHostToDevice, st));
         PHD_HIP(launch_hsv_stats_batch((const uint8_t* const*)(dw + L.P_dev(n)), n, height, width, gp, cls->fc,
                                        cls->d, pd, (long)L.a_bytes, (long)L.chunk_bytes, nchunks, c->d_k255,
                                        true, fused, all_aligned(d_imgs, n), st));
@@ -345,7 +348,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                   " px is not supported by this build's LDS-resident FFT");
         return false;
     }
-    const hipStream_t st = stream ? stream : c->stream;
+    const hipStream_t st = work_stream(c, stream);
     while ((int)c->ev_img_fft.size() < n) {
         hipEvent_t a, b;
         PHD_HIP(hipEventCreateWithFlags(&a, hipEventDisableTiming));
@@ -459,7 +462,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             c->prof.end(ps, sf);
             PHD_HIP(hipEventRecord(c->ev_rows[b], sf));
             PHD_HIP(hipStreamWaitEvent(sc, c->ev_rows[b], 0));
-            double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
+            auto* bins = (unsigned long long*)(dw + L.C(n, i) + L.c_bins);
             double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
             ps = c->prof.begin(kFftCols, sc);
             PHD_HIP(launch_cols_sel(fs, inter, height, width, wf, tbl->d_map, nbins, bins, fmx, sums, nullptr, sc));
@@ -484,7 +487,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         c->prof.end(ps, sf);
         ps = c->prof.begin(kFftCols, sf);
         PHD_HIP(launch_fft_cols_batch(c->d_inter, inter_elems, g1 - g0, height, wf, fs.pcol->plan, tbl->d_map, nbins,
-                                      (double*)(dw + L.C(n, g0) + L.c_bins), (double*)(dw + L.C(n, g0) + L.c_fmax),
+                                      (unsigned long long*)(dw + L.C(n, g0) + L.c_bins),
+                                      (double*)(dw + L.C(n, g0) + L.c_fmax),
                                       (long)(L.c_bytes / 8), sf));
         c->prof.end(ps, sf);
         for (int i = g0; i < g1; i++) {
@@ -510,7 +514,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = own_dc ? (const unsigned long long*)(dw + L.C(n, i) + L.c_rsum)
                                                     : (const unsigned long long*)(dw + L.A(i) + L.a_sums);
-            double* bins = (double*)(dw + L.C(n, i) + L.c_bins);
+            auto* bins = (unsigned long long*)(dw + L.C(n, i) + L.c_bins);
             double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
             const int ps = c->prof.begin(kFftCols, sf);
             PHD_HIP(launch_cols_sel(fs, c->d_inter + (size_t)(i - g0) * inter_elems, height, width, wf, tbl->d_map,
@@ -689,7 +693,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         }
         std::string w;
         out[i] = assemble(st_i, s_acc / (double)n_hsv, dec[i], pal, n_hsv, *tbl,
-                          (const double*)(cc + L.c_bins), fmax, cfg, crops,
+                          (const unsigned long long*)(cc + L.c_bins), fmax, cfg, crops,
                           (const double*)(cc + L.c_sharp), &w);
         if (!out[i]) {
             set_error(w);
@@ -711,6 +715,17 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                     ms_between(c->ev[2], c->ev[3]), ms_between(c->ev[0], c->ev[4]), ms(t_host0, t_end),
                     ms(t_host0, t_enq), ms(t_k1, t_dec), ms(t_sync, t_end)};
     record_timings(tm, 8);
+    static const bool verbose = getenv("PHD_VERBOSE") != nullptr;
+    if (verbose) {
+        // END_TIMING's format (src/utilities.h:12-18), one line per stage of this
+        // pipeline (the device stages are HIP-event spans of the whole batch)
+        const char* names[8] = {"rgb2hsv + rgb statistics + hsv average + palette histogram (K1)",
+                                "rgb2pgm + fft + blur profile (FFT rows + columns)",
+                                "color palette (second pass after the FFTs)", "device total",
+                                "full report (host wall clock)", "enqueue", "color palette decisions",
+                                "compile full report"};
+        for (int k = 0; k < 8; k++) printf("%s took %f seconds to execute \n", names[k], tm[k] / 1e3);
+    }
     return failures == 0;
 }
 
@@ -956,7 +971,7 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
     Context* c = get_context();
     if (!c) return -1;
     std::lock_guard<std::mutex> lk(c->mu);
-    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const hipStream_t st = work_stream(c, stream);
     const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
     const long npix = (long)height * width;
     const int nchunks = (int)((npix + kChunk - 1) / kChunk);
@@ -1025,7 +1040,7 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
     Context* c = get_context();
     if (!c) return -1;
     std::lock_guard<std::mutex> lk(c->mu);
-    const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const hipStream_t st = work_stream(c, stream);
     const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
     std::vector<const uint8_t*> imgs(n_images);
     for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
@@ -1082,7 +1097,8 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
         c->prof.end(ps, st);
         ps = c->prof.begin(kFftCols, st);
         if ((e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map, nbins,
-                                 (double*)(dw + (size_t)i * rb + r_bins), (double*)(dw + (size_t)i * rb + r_fmax),
+                                 (unsigned long long*)(dw + (size_t)i * rb + r_bins),
+                                 (double*)(dw + (size_t)i * rb + r_fmax),
                                  sums, nullptr, st)) != hipSuccess)
             return fail(e, "column pass");
         c->prof.end(ps, st);
@@ -1096,7 +1112,7 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
         const double* fpart = (const double*)(r + r_fmax);
         double fmax = 0.0;
         for (int b = 0; b < fs.col_blocks; b++) fmax = fpart[b] > fmax ? fpart[b] : fmax;
-        finish_blur(*tbl, (const double*)(r + r_bins), fmax, *cfg, bins_out + (size_t)i * nbins,
+        finish_blur(*tbl, (const unsigned long long*)(r + r_bins), fmax, *cfg, bins_out + (size_t)i * nbins,
                     vectors_out + (size_t)i * 10);
     }
     return 0;
@@ -1245,7 +1261,7 @@ extern "C" int phd_fill_uniform_device(uint8_t* d_dst, size_t n, uint64_t seed, 
     clear_error();
     Context* c = get_context();
     if (!c) return -1;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = work_stream(c, stream);
     if (launch_fill_uniform(d_dst, n, seed, st) != hipSuccess) {
         set_error("fill kernel launch failed");
         return -1;
@@ -1347,7 +1363,8 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
                 break;
             case kFftRows: e = launch_rows_sel(fs, d_rgb, height, width, pd.sums, c->d_k255, c->d_inter, st); break;
             case kFftCols: e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map,
-                                               cfg->radius_partitions * cfg->angle_partitions, (double*)pd.chunk_hist,
+                                               cfg->radius_partitions * cfg->angle_partitions,
+                                               (unsigned long long*)pd.chunk_hist,
                                                (double*)pd.chunk_hist + 65536, pd.sums, nullptr, st); break;
             default: set_error("kernel not supported by the timing hook"); g_ablate = 0; return -1;
         }
@@ -1398,10 +1415,11 @@ extern "C" int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int wi
     const int wf = width / 2 + 1;
     double* scratch = nullptr;
     if (hipMalloc(&scratch, sizeof(double) * (nbins + 4096)) != hipSuccess) return -1;
+    auto* scratch_bins = reinterpret_cast<unsigned long long*>(scratch);
     const hipStream_t st = c->stream;
     hipError_t e = launch_rows_sel(fs, d_rgb, height, width, (const unsigned long long*)dw, c->d_k255, c->d_inter, st);
     if (e == hipSuccess)
-        e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map, nbins, scratch, scratch + nbins,
+        e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map, nbins, scratch_bins, scratch + nbins,
                             (const unsigned long long*)dw, d_out, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(scratch);

@@ -48,16 +48,28 @@ def loads(sizes: Sequence[Tuple[int, int]], plan: List[List[int]]) -> List[int]:
     return [sum(sizes[i][0] * sizes[i][1] for i in idx) for idx in plan]
 
 
-def merge_counters(elapsed_s: float, images: float, pixels: float, device=None):
-    """The single collective: max of wall time, sum of images and pixels over
-    the default process group (identity when torch.distributed is not
-    initialised).  Returns (elapsed_max, images_total, pixels_total)."""
+COUNTERS = ("elapsed", "images", "pixels", "alg_bytes", "kernel_ms", "launches")
+
+
+def merge_counters(values, device=None):
+    """The single collective: one all-gather of this rank's
+    counter vector {elapsed s, images, pixels, algorithmic bytes, kernel ms,
+    kernel launches} over the default process group (RCCL over xGMI on the GPU
+    box, gloo in the CPU tests; identity when torch.distributed is not
+    initialised).  Every rank gets the merge: the max of the wall times and the
+    sums of the rest, plus each rank's wall time (per_rank_elapsed)."""
     import torch
     import torch.distributed as dist
-    t = torch.tensor([elapsed_s, images, pixels], dtype=torch.float64, device=device)
+    vals = [float(v) for v in values] + [0.0] * (len(COUNTERS) - len(values))
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        mx = t[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        t[0] = mx[0]
-    return float(t[0]), float(t[1]), float(t[2])
+        out = torch.empty(dist.get_world_size() * len(COUNTERS), dtype=torch.float64, device=device)
+        dist.all_gather_into_tensor(out, t)
+        out = out.view(-1, len(COUNTERS))
+    else:
+        out = t[None]
+    rows = out.cpu().tolist()
+    res = {k: sum(r[j] for r in rows) for j, k in enumerate(COUNTERS)}
+    res["elapsed"] = max(r[0] for r in rows)
+    res["per_rank_elapsed"] = [r[0] for r in rows]
+    return res

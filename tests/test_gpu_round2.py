@@ -1,0 +1,91 @@
+"""GPU tests added in round 2: determinism of the blur bins, stream ordering with
+PyTorch producers, and batched runtime-plan sizes with downsample_rate > 1.
+
+Every test calls through the C-ABI (libreport_data.so); the oracle is only
+the checker.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _phd():
+    import torch
+    import photohive_dsp_amd as phd
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return phd, torch
+
+
+def _bins(rep):
+    return np.array(rep.blur_profile.bins)
+
+
+@pytest.mark.parametrize("kind,h,w", [("structured", 3000, 4000), ("symmetric", 512, 512), ("hblur", 720, 1280)])
+def test_blur_bins_bit_identical_over_repeats(kind, h, w):
+    """vectorize_blur_profile (src/blur_profile.c:324-416) thresholds the bins with
+    strict comparisons, so they must not move between runs: the column pass sums
+    them as fixed-point integers (order-independent atomics).  10 runs of the same
+    image in one process give bit-identical bins and vectors."""
+    phd, torch = _phd()
+    from photohive_dsp_amd import synth
+    if kind == "symmetric":
+        # mirror-symmetric in both axes: many exactly equal bins and ties
+        q = synth.structured(h // 2, w // 2, 9)
+        img = np.ascontiguousarray(np.concatenate([np.concatenate([q, q[:, ::-1]], 1),
+                                                   np.concatenate([q[::-1], q[::-1, ::-1]], 1)], 0))
+    else:
+        img = synth.make(kind, h, w, 31)
+    t = torch.from_numpy(img).cuda()[None].contiguous()
+    first = phd.report_device(t)[0]
+    b0, v0 = _bins(first), [(v.angle, v.magnitude) for v in first.blur_vectors]
+    for _ in range(9):
+        r = phd.report_device(t)[0]
+        assert np.array_equal(_bins(r), b0)
+        assert [(v.angle, v.magnitude) for v in r.blur_vectors] == v0
+    # the host-buffer path gives the same bits
+    r = phd.get_report(img)
+    assert np.array_equal(_bins(r), b0)
+
+
+def test_device_input_produced_by_async_torch_op():
+    """A device image still being produced on PyTorch's (null) stream when the
+    call is made: the library orders its stream after it (work_stream)."""
+    phd, torch = _phd()
+    from photohive_dsp_amd import synth
+    img = synth.structured(600, 800, 5)
+    src = torch.from_numpy(img).cuda()
+    torch.cuda.synchronize()
+    a = torch.randn(6144, 6144, device="cuda")
+    for _ in range(4):
+        a = a @ a                                   # keeps the stream busy for milliseconds
+        a = a / a.abs().max()
+    t = (src.to(torch.int16) + (a[0, 0] * 0).to(torch.int16)).to(torch.uint8)[None].contiguous()
+    r = phd.report_device(t)[0]
+    ref = phd.get_report(img)
+    assert r.color_palette.group_ids == ref.color_palette.group_ids
+    assert r.color_palette.quantities == ref.color_palette.quantities
+    assert np.array_equal(_bins(r), _bins(ref))
+
+
+@pytest.mark.parametrize("shape", [(512, 512), (513, 700)])
+def test_batched_runtime_plan_with_downsample(shape):
+    """Two same-size images without a compile-time FFT plan at downsample_rate 2:
+    the batched row pass reads the device pointer array, which must be uploaded
+    on this path too (it used to be stale).  Each report equals the single-image
+    report and the oracle."""
+    phd, torch = _phd()
+    from oracle import oracle as orc
+    from photohive_dsp_amd import synth
+    h, w = shape
+    imgs = [synth.make("structured", h, w, 61), synth.make("uniform", h, w, 62)]
+    reps = phd.get_reports(imgs, downsample_rate=2)
+    for img, r in zip(imgs, reps):
+        one = phd.get_report(img, downsample_rate=2)
+        assert r.color_palette.group_ids == one.color_palette.group_ids
+        assert r.color_palette.quantities == one.color_palette.quantities
+        assert np.array_equal(_bins(r), _bins(one))
+        o = orc.report(img, downsample_rate=2)
+        np.testing.assert_array_equal(np.array(r.color_palette.group_ids), o.valid_parents)
+        np.testing.assert_array_equal(np.array(r.color_palette.quantities), o.palette_pct)
+        np.testing.assert_allclose(_bins(r), o.bins, rtol=1e-4, atol=1e-12)

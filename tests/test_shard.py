@@ -50,7 +50,10 @@ def _worker(rank, world, port, q):
         plan = shard.assign(sizes, world)
         mine = plan[rank]
         pix = sum(sizes[i][0] * sizes[i][1] for i in mine)
-        el, n, p = shard.merge_counters(0.5 + rank, float(len(mine)), float(pix))
+        m = shard.merge_counters([0.5 + rank, float(len(mine)), float(pix), 3.0 * pix])
+        el, n, p = m["elapsed"], m["images"], m["pixels"]
+        assert m["alg_bytes"] == 3.0 * sum(h * w for h, w in sizes)
+        assert m["per_rank_elapsed"] == [0.5 + r for r in range(world)]
         got = [None] * world
         dist.all_gather_object(got, mine)
         q.put((rank, el, n, p, got))
