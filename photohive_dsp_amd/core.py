@@ -94,9 +94,10 @@ class Report:
         bp = SimpleNamespace()
         bins = [list(ctypes.cast(c.bins[i], POINTER(ctypes.c_double * c.num_radius_bins)).contents)
                 for i in range(c.num_angle_bins)]
-        for a, row in enumerate(bins):            # core.py:109-117
+        for a, row in enumerate(bins):            # core.py:109-117, same message
             for r, val in enumerate(row):
                 if np.isnan(val):
+                    print(f"NaN found at angle {a}, radius {r}. Correcting to 0.")
                     bins[a][r] = 0.0
         bp.bins = bins
         return bp

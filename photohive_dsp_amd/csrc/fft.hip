@@ -296,7 +296,8 @@ template <int T, bool GEN>
 __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inter0, size_t inter_stride, int H,
                                                 int wf, int C, FftPlan plan, const uint16_t* __restrict__ binmap,
                                                 int nbins, int lds_bins, unsigned long long* __restrict__ bin_sums0,
-                                                double* __restrict__ fmax_part0, long out_stride, int ablate) {
+                                                double* __restrict__ fmax_part0, long out_stride, double bscale,
+                                                int ablate) {
     // blockIdx.y: the image of a batch (inter0 + y * inter_stride elements,
     // bin sums and max partials at + y * out_stride doubles)
     const double2* inter = inter0 + (size_t)blockIdx.y * inter_stride;
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
             if (p >= 1) {                               // fft_processing.c:197-198
                 const int c = i / H, u = i - c * H;
                 b = binmap[(size_t)(k0 + c) * H + u];
-                lg = bin_fixed(log(p));
+                lg = bin_fixed(log(p), bscale);
             }
         }
         // fixed-point integers: the sums do not depend on the atomics' order
@@ -420,7 +421,8 @@ static hipError_t cols_impl(const double2* inter, size_t inter_stride, int n, in
     (void)once;
     static const int ablate = getenv("PHD_ABLATE") ? atoi(getenv("PHD_ABLATE")) : 0;   // debug only
     phd_launch((k_fft_cols<T, GEN>), dim3((wf + C - 1) / C, n), dim3(T), lds, st, inter, inter_stride, height,
-                       wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_part, out_stride, ablate);
+                       wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_part, out_stride, bin_scale(height, wf),
+                       ablate);
     return hipGetLastError();
 }
 

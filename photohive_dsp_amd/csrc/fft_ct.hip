@@ -263,7 +263,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                                                      unsigned long long* __restrict__ bin_sums, double* __restrict__ fmax_part,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums, int width,
-                                                     double* __restrict__ dbg, int ablate_arg) {
+                                                     double* __restrict__ dbg, double bscale, int ablate_arg) {
     using K = ColK<H, T, CPB, Rs...>;
     constexpr int NC = K::NC;
     const int ablate = PHD_ABL(ablate_arg);
@@ -384,7 +384,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         }
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
-        // few tens of rows along a column), in kBinScale fixed point so that the
+        // few tens of rows along a column), in bin_scale fixed point so that the
         // sums do not depend on the order of the atomics
         if (!(ablate & 2)) {
             int cur = -1;
@@ -397,7 +397,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     if (lg >= 0.0) {
                         const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
                         if (bin != cur) {
-                            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc));
+                            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc, bscale));
                             cur = bin;
                             acc = 0.0;
                         }
@@ -405,7 +405,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     }
                 }
             }
-            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc));
+            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc, bscale));
         }
         __syncthreads();
     }
@@ -469,7 +469,8 @@ hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binm
                    hipStream_t st) {
     const size_t lds = ColK<H, T, CPB, Rs...>::lds(nbins);
     phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3((CPB & 3) * T), lds,
-                       st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, g_ablate);
+                       st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf),
+                       g_ablate);
     return hipGetLastError();
 }
 

@@ -316,8 +316,8 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
-// a non-negative sum of log(p) as kBinScale fixed point (round to nearest)
-__device__ __forceinline__ unsigned long long bin_fixed(double x) { return __double2ull_rn(x * kBinScale); }
+// a non-negative sum of log(p) as bin_scale fixed point (round to nearest)
+__device__ __forceinline__ unsigned long long bin_fixed(double x, double scale) { return __double2ull_rn(x * scale); }
 
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll

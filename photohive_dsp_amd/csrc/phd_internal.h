@@ -30,13 +30,18 @@ constexpr int kThreads = 256;
 constexpr int kFftMaxLds = 8192;
 constexpr int kMaxFftPasses = 24;
 // Polar-bin sums of log(p) are accumulated as unsigned 64-bit fixed point
-// (value * 2^32): integer additions commute, so the bins -- and the strict
-// threshold comparisons vectorize_blur_profile makes on them -- are the same
-// on every run whatever order the atomics land in.  A bin's sum stays below
-// 60M elements x log(1.5e16) = 2.2e9 < 2^31 for any image the reference
-// accepts (120 MP), so it fits; one run's rounding is <= 2^-33.
-constexpr double kBinScale = 4294967296.0;
-constexpr double kBinInvScale = 1.0 / 4294967296.0;
+// (value * bin_scale): integer additions commute, so the bins -- and the
+// strict threshold comparisons vectorize_blur_profile makes on them -- are the
+// same on every run whatever order the atomics land in.  The scale is the
+// largest power of two that keeps any bin of an H x Wf half spectrum below
+// 2^62: |X| <= N = H * W (pgm values lie in [0, 1]), so log p <= 2 ln N and a
+// bin holds at most H * Wf elements (2^-35 per element at 4000x3000, 2^-41
+// at 640x480; 2^-30 at the reference's 120 MP limit).
+inline double bin_scale(int height, int wf) {
+    const double n = (double)height * (2.0 * wf);
+    const double bound = (double)height * wf * 2.0 * __builtin_log(n > 2.0 ? n : 2.0) + 1.0;
+    return __builtin_ldexp(1.0, 62 - (int)__builtin_ceil(__builtin_log2(bound)));
+}
 
 // The HSV grid of initialize_octree (src/color_quantization.c:22-101).
 struct GridParams {
@@ -211,7 +216,7 @@ hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftP
                            double2* inter, hipStream_t st);
 // Column pass + epilogue: power, running max, sum log(p) over p >= 1 per
 // polar bin (binmap[wf][height], uint16 bin ids).  Accumulates into
-// bin_sums[na*nr] (kBinScale fixed point) and writes one max power per block to fmax_part.
+// bin_sums[na*nr] (bin_scale fixed point) and writes one max power per block to fmax_part.
 hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
                            const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
                            double* fmax_part, hipStream_t st);

@@ -133,10 +133,11 @@ void finish_blur(const BlurTable& tbl, const unsigned long long* bin_sums, doubl
                  double* flat, Blur_Vector* vectors) {
     const int na = cfg.angle_partitions, nr = cfg.radius_partitions;
     const double gs = 1 / (2 * std::log(std::sqrt(fmax) + 1));
+    const double scale = bin_scale(tbl.height, tbl.wf);
     for (size_t b = 0; b < (size_t)na * nr; b++) {
         const double q = (double)tbl.counts[b];
-        // the device sums are kBinScale fixed point (order-independent)
-        const double sum = bin_sums[b] == 0ull ? 0.0 : (double)bin_sums[b] * kBinInvScale * gs;
+        // the device sums are bin_scale fixed point (order-independent)
+        const double sum = bin_sums[b] == 0ull ? 0.0 : (double)bin_sums[b] / scale * gs;
         flat[b] = q != 0 ? sum / q : 0;
     }
     vectorize_blur(flat, na, nr, cfg.fft_streak_thresh, cfg.magnitude_thresh, cfg.blur_cutoff_ratio_denom, vectors);

@@ -1,7 +1,7 @@
 """Generate the golden fixtures in tests/golden/ from the REFERENCE's own C.
 
 Run in the build container only (needs /root/reference and `make -C oracle ref`):
-    python -m tests.golden.make_golden
+    python -m tests.golden.make_golden [--only name,name,...]
 
 Each case stores its input as a generator spec (photohive_dsp_amd.synth) and
 the reference outputs of oracle/ref_pipeline.py (the reference's own functions
@@ -19,6 +19,8 @@ from oracle import ref_pipeline as rp
 from photohive_dsp_amd import synth
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+
+HSV36 = {"h_partitions": 36, "s_partitions": 4, "v_partitions": 5}
 
 CASES = [
     # name, kind, H, W, seed, config overrides, crops
@@ -45,15 +47,61 @@ CASES = [
     ("structured_crops_600x800", "structured", 600, 800, 15, {},
      [dict(top=10, bottom=210, left=20, right=320), dict(top=300, bottom=599, left=400, right=799),
       dict(top=0, bottom=600, left=0, right=800)]),
+    # round 2: the 12 MP saliency INT_MIN ordering (compare_quantities' cvttss2si,
+    # src/color_quantization.c:601-611: the 51 % colour is sorted 2nd) ...
+    ("dominant_3000x4000_intmin", "dominant", 3000, 4000, 1, {}, None),
+    # ... and BASELINE config 5's shapes at h/s/v 36/4/5 not covered above
+    ("uniform_1536x2048_hsv36", "uniform", 1536, 2048, 21, HSV36, None),
+    ("structured_640x480_hsv36", "structured", 640, 480, 22, HSV36, None),
+    ("dominant_1280x720_hsv36", "dominant", 1280, 720, 23, HSV36, None),
+    ("structured_3000x4000_hsv36", "structured", 3000, 4000, 24, HSV36, None),
 ]
+
+# get_blur_profile_visual (src/blur_profile.c:140-180) on a Blur_Profile whose
+# bins hold their own index a * nr + r: the output is the (phi_bin, r_bin)
+# lookup of every pixel, stored as uint16 (H, W, na, nr, radius_bin_size)
+VISUAL = [(480, 640, 72, 40, 10), (401, 577, 72, 40, 8), (512, 512, 36, 20, 18), (600, 800, 72, 40, 12),
+          (577, 401, 7, 3, 111)]
 
 ERROR_SHAPES = [(349, 350), (350, 349), (2001, 400), (400, 2001), (120000, 10000), (350, 350),
                 (400, 2000), (2000, 400), (10000, 12000)]
 
 
-def main():
+def visual_fixture():
+    import ctypes as C
+    L = rp.lib()
+    out = {}
+    for h, w, na, nr, rbs in VISUAL:
+        rows = [(C.c_double * nr)(*[float(a * nr + r) for r in range(nr)]) for a in range(na)]
+        ptrs = (C.POINTER(C.c_double) * na)(*[C.cast(r, C.POINTER(C.c_double)) for r in rows])
+        bp = rp.Blur_Profile(na, nr, 180 // na, rbs, ptrs)
+        img = L.get_blur_profile_visual(C.byref(bp), h, w)
+        data = np.ctypeslib.as_array(img.contents.data, shape=(h * w,)).copy()
+        L.free_image_pgm(img)
+        assert np.all(data == np.rint(data)) and data.max() < 65536
+        out[f"{h}x{w}_{na}_{nr}_{rbs}"] = data.reshape(h, w).astype(np.uint16)
+    np.savez_compressed(os.path.join(HERE, "blur_visual.npz"), **out)
+    print("wrote blur_visual", flush=True)
+
+
+def main(argv=None):
+    import sys
+    argv = sys.argv[1:] if argv is None else argv
+    only = None
+    if "--only" in argv:
+        only = set(argv[argv.index("--only") + 1].split(","))
+    path = os.path.join(HERE, "manifest.json")
+    old = {}
+    if only is not None and os.path.exists(path):
+        with open(path) as f:
+            old = {c["name"]: c for c in json.load(f)["cases"]}
     manifest = {"cases": [], "errors": []}
     for name, kind, h, w, seed, kw, crops in CASES:
+        entry = dict(name=name, kind=kind, height=h, width=w, seed=seed, config=kw, crops=crops)
+        manifest["cases"].append(entry)
+        if only is not None and name not in only:
+            assert name in old, f"{name} has no fixture yet"
+            continue
         img = synth.make(kind, h, w, seed)
         r = rp.report(img, rp.Config(**kw), crops=crops)
         arrays = dict(stats=r.stats, average_saturation=np.array(r.average_saturation), hist=r.hist,
@@ -67,13 +115,13 @@ def main():
         if r.sharpness is not None:
             arrays["sharpness"] = r.sharpness
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
-        manifest["cases"].append(dict(name=name, kind=kind, height=h, width=w, seed=seed, config=kw,
-                                      crops=crops))
         print("wrote", name, flush=True)
     for h, w in ERROR_SHAPES:
         manifest["errors"].append(dict(height=h, width=w, rejected=rp.error_check(h, w)))
-    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(manifest, f, indent=1)
+    if only is None or "blur_visual" in only:
+        visual_fixture()
     print("manifest written")
 
 
