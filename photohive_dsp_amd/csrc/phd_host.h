@@ -121,6 +121,7 @@ private:
     unsigned gen_ = 0;
 };
 HostPool* host_pool();
+HostPool* copy_pool();   // threads for host-buffer staging copies (phd_upload.cpp)
 
 struct Context {
     int device = -1;
@@ -167,6 +168,16 @@ struct Context {
     std::vector<hipEvent_t> ev_img_fft, ev_img_dl;
     KernelProfiler prof;
     hipEvent_t ev_null = nullptr;                   // orders the library stream after the null stream
+    // host-buffer uploads (phd_upload.cpp): pinned slot ring on the h2d stream,
+    // two device staging buffers for overlapping groups
+    hipStream_t h2d = nullptr;
+    uint8_t* h2d_slots = nullptr;
+    std::vector<hipEvent_t> ev_slot;
+    std::vector<char> slot_used;
+    int next_slot = 0;
+    hipEvent_t ev_up[2] = {};
+    uint8_t* d_stage2[2] = {};
+    size_t stage2_bytes[2] = {};
     std::mutex mu;
 };
 // The context of the current HIP device (created on first use).  nullptr if no GPU.
@@ -218,5 +229,11 @@ bool run_palette_trace(Context* c, const uint8_t* d_img, int height, int width, 
                        std::vector<double>* device_counts);
 
 void record_timings(const double* ms, int n);
+
+// ---- host-buffer uploads (phd_upload.cpp) -------------------------------------
+bool upload_init(Context* c);
+// Copy `bytes` host bytes to d_dst through the pinned slot ring on c->h2d.  On
+// return the caller's buffer has been read; the DMA may still run.
+bool upload_async(Context* c, uint8_t* d_dst, const uint8_t* src, size_t bytes, std::string* why);
 
 }  // namespace phd

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <unistd.h>
 
 #include "phd_host.h"
@@ -842,14 +843,23 @@ static Full_Report_Data* report_from_host(const uint8_t* rgb, int height, int wi
     std::lock_guard<std::mutex> lk(c->mu);
     const size_t row = 3 * (size_t)width;
     const size_t bytes = row * height;
-    if (!ensure_device((void**)&c->d_stage, &c->stage_bytes, bytes)) return nullptr;
-    hipError_t e;
-    if (row_stride == 0 || row_stride == row)
-        e = hipMemcpyAsync(c->d_stage, rgb, bytes, hipMemcpyHostToDevice, c->stream);
-    else
-        e = hipMemcpy2DAsync(c->d_stage, row, rgb, row_stride, row, height, hipMemcpyHostToDevice, c->stream);
-    if (e != hipSuccess) {
-        set_error(std::string("upload failed: ") + hipGetErrorString(e));
+    if (!ensure_device((void**)&c->d_stage, &c->stage_bytes, bytes) || !upload_init(c)) return nullptr;
+    if (row_stride == 0 || row_stride == row) {
+        std::string why;
+        if (!upload_async(c, c->d_stage, rgb, bytes, &why)) {
+            set_error(why);
+            return nullptr;
+        }
+    } else {
+        const hipError_t e = hipMemcpy2DAsync(c->d_stage, row, rgb, row_stride, row, height, hipMemcpyHostToDevice,
+                                              c->h2d);
+        if (e != hipSuccess) {
+            set_error(std::string("upload failed: ") + hipGetErrorString(e));
+            return nullptr;
+        }
+    }
+    if (hipEventRecord(c->ev_up[0], c->h2d) != hipSuccess || hipStreamWaitEvent(c->stream, c->ev_up[0], 0) != hipSuccess) {
+        set_error("upload ordering failed");
         return nullptr;
     }
     const uint8_t* imgs[1] = {c->d_stage};
@@ -857,6 +867,7 @@ static Full_Report_Data* report_from_host(const uint8_t* rgb, int height, int wi
     int status = -1;
     run_reports(c, imgs, 1, height, width, *cfg, crops, &out, &status, nullptr);
     // the caller's buffer may be freed on return: drain the upload on every path
+    (void)hipStreamSynchronize(c->h2d);
     (void)hipStreamSynchronize(c->stream);
     return out;
 }
@@ -1168,7 +1179,9 @@ extern "C" int phd_report_batch_device_mixed(const uint8_t* const* d_images, con
 }
 
 // Host images of any sizes: each same-size group (<= 16) is uploaded into one
-// device staging buffer and reported as one batch.
+// of two device staging buffers and reported as one batch; the next group's
+// upload (pinned slot ring, copy threads + DMA) runs on an uploader thread
+// while the current group computes.
 extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heights, const int* widths,
                                    int n_images, const phd_config* cfg, Full_Report_Data** out, int* status) {
     clear_error();
@@ -1187,37 +1200,59 @@ extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heig
     Context* c = get_context();
     if (!c) return -1;
     std::lock_guard<std::mutex> lk(c->mu);
+    if (!upload_init(c)) return -1;
+    std::vector<std::vector<int>> groups;
+    for (auto& g : size_groups(heights, widths, n_images, 16)) {
+        if (precheck(heights[g[0]], widths[g[0]])) groups.push_back(std::move(g));
+    }
     int fails = 0;
-    for (const auto& grp : size_groups(heights, widths, n_images, 16)) {
-        const int m = (int)grp.size(), h = heights[grp[0]], w = widths[grp[0]];
-        if (!precheck(h, w)) {
-            fails += m;
-            continue;
+    // device buffers first (the uploader thread must not allocate)
+    size_t need = 0;
+    for (const auto& g : groups) need = std::max(need, g.size() * 3 * (size_t)widths[g[0]] * heights[g[0]]);
+    for (int b = 0; b < 2 && !groups.empty(); b++)
+        if (!ensure_device((void**)&c->d_stage2[b], &c->stage2_bytes[b], need)) return -1;
+    struct Up {
+        bool ok = true;
+        std::string why;
+    };
+    auto upload = [c, images, heights, widths](const std::vector<int>& g, int b, Up* u) {
+        const size_t bytes = 3 * (size_t)widths[g[0]] * heights[g[0]];
+        for (size_t k = 0; k < g.size() && u->ok; k++)
+            u->ok = upload_async(c, c->d_stage2[b] + k * bytes, images[g[k]], bytes, &u->why);
+        if (u->ok && hipEventRecord(c->ev_up[b], c->h2d) != hipSuccess) {
+            u->ok = false;
+            u->why = "upload event failed";
         }
+    };
+    std::vector<Up> ups(groups.size());
+    std::thread th;
+    if (!groups.empty()) th = std::thread(upload, std::cref(groups[0]), 0, &ups[0]);
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+        th.join();                                   // group gi is enqueued (its host buffers are read)
+        const auto& g = groups[gi];
+        const int b = (int)(gi & 1);
+        // the next group's upload runs under this group's reports (its buffer's
+        // previous group finished: run_reports returns after the GPU is done)
+        if (gi + 1 < groups.size()) th = std::thread(upload, std::cref(groups[gi + 1]), 1 - b, &ups[gi + 1]);
+        const int m = (int)g.size(), h = heights[g[0]], w = widths[g[0]];
         const size_t bytes = 3 * (size_t)w * h;
-        if (!ensure_device((void**)&c->d_stage, &c->stage_bytes, (size_t)m * bytes)) return -1;
         std::vector<const uint8_t*> ptrs(m);
-        bool up = true;
-        for (int k = 0; k < m && up; k++) {
-            ptrs[k] = c->d_stage + (size_t)k * bytes;
-            const hipError_t e = hipMemcpyAsync((void*)ptrs[k], images[grp[k]], bytes, hipMemcpyHostToDevice,
-                                                c->stream);
-            if (e != hipSuccess) {
-                set_error(std::string("upload failed: ") + hipGetErrorString(e));
-                up = false;
-            }
-        }
+        for (int k = 0; k < m; k++) ptrs[k] = c->d_stage2[b] + (size_t)k * bytes;
         std::vector<Full_Report_Data*> o(m, nullptr);
         std::vector<int> st(m, -1);
-        if (up) run_reports(c, ptrs.data(), m, h, w, *cfg, nullptr, o.data(), st.data(), nullptr);
-        // the caller's buffers may be freed on return: drain the uploads
-        (void)hipStreamSynchronize(c->stream);
+        if (!ups[gi].ok) set_error(ups[gi].why);
+        else if (hipStreamWaitEvent(c->stream, c->ev_up[b], 0) != hipSuccess) set_error("upload ordering failed");
+        else run_reports(c, ptrs.data(), m, h, w, *cfg, nullptr, o.data(), st.data(), nullptr);
         for (int k = 0; k < m; k++) {
-            out[grp[k]] = o[k];
-            status[grp[k]] = st[k];
-            fails += st[k] != 0;
+            out[g[k]] = o[k];
+            status[g[k]] = st[k];
         }
     }
+    if (th.joinable()) th.join();
+    // the caller's buffers may be freed on return: every transfer has completed
+    (void)hipStreamSynchronize(c->h2d);
+    (void)hipStreamSynchronize(c->stream);
+    for (int i = 0; i < n_images; i++) fails += status[i] != 0;
     return fails;
 }
 

@@ -1,0 +1,96 @@
+// phd_upload.cpp -- host RGB8 buffers to device memory, pipelined.
+//
+// The timed region of SURVEY.md 8(d) starts from a u8 HOST buffer.  The
+// caller's buffers are pageable (a numpy array, a decoded image).  By default
+// they go to the device through the HIP runtime's own pageable path on the
+// `h2d` stream (measured 1434 images/s = 51.6 GB/s for 64 x 4000x3000 through
+// phd_report_batch_u8, against 1360 for the ring below).  PHD_UPLOAD=staged
+// selects an explicit ring: each image is cut into 16 MB chunks that rotate
+// through pinned slots, copy threads filling slot j while the DMA engine sends
+// slot j - 1.
+//
+// phd_report_batch_u8 runs the uploads of the next same-size group on an
+// uploader thread while the current group's reports compute (two device
+// staging buffers), so the H2D traffic overlaps the GPU work.
+#include <cstring>
+#include <thread>
+
+#include <unistd.h>
+
+#include "phd_host.h"
+
+namespace phd {
+
+namespace {
+constexpr size_t kSlotBytes = (size_t)16 << 20;
+constexpr int kSlots = 8;
+}  // namespace
+
+HostPool* copy_pool() {
+    // the palette decisions own host_pool(); the copies get their own threads
+    static std::mutex m;
+    static HostPool* p = nullptr;
+    static pid_t owner = 0;
+    std::lock_guard<std::mutex> lk(m);
+    if (!p || owner != getpid()) {
+        const unsigned hc = std::thread::hardware_concurrency();
+        p = new HostPool(hc > 2 ? (int)std::min(hc - 1, 7u) : 0);
+        owner = getpid();
+    }
+    return p;
+}
+
+bool upload_init(Context* c) {
+    if (c->h2d) return true;
+    if (hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void**)&c->h2d_slots, kSlotBytes * kSlots, hipHostMallocDefault) != hipSuccess) {
+        set_error("upload staging setup failed");
+        return false;
+    }
+    c->ev_slot.resize(kSlots);
+    for (auto& e : c->ev_slot)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    c->slot_used.assign(kSlots, 0);
+    for (auto& e : c->ev_up)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    return true;
+}
+
+// Enqueue the transfer of `bytes` contiguous host bytes to d_dst on c->h2d.
+// Returns once every chunk has been copied into a pinned slot (the caller's
+// buffer is no longer read); the DMA may still be running.
+bool upload_async(Context* c, uint8_t* d_dst, const uint8_t* src, size_t bytes, std::string* why) {
+    static const bool staged = getenv("PHD_UPLOAD") && !strcmp(getenv("PHD_UPLOAD"), "staged");
+    if (!staged) {   // the HIP runtime's own pageable path (faster, measured)
+        const hipError_t e = hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, c->h2d);
+        if (e != hipSuccess) *why = std::string("upload failed: ") + hipGetErrorString(e);
+        return e == hipSuccess && hipStreamSynchronize(c->h2d) == hipSuccess;
+    }
+    HostPool* pool = copy_pool();
+    for (size_t off = 0; off < bytes; off += kSlotBytes) {
+        const int s = c->next_slot;
+        c->next_slot = (c->next_slot + 1) % kSlots;
+        if (c->slot_used[s] && hipEventSynchronize(c->ev_slot[s]) != hipSuccess) {
+            *why = "upload: slot event failed";
+            return false;
+        }
+        const size_t n = std::min(kSlotBytes, bytes - off);
+        uint8_t* slot = c->h2d_slots + (size_t)s * kSlotBytes;
+        constexpr size_t piece = (size_t)1 << 20;
+        const int np = (int)((n + piece - 1) / piece);
+        pool->parallel_for(np, [&](int k) {
+            const size_t o = (size_t)k * piece;
+            memcpy(slot + o, src + off + o, std::min(piece, n - o));
+        });
+        hipError_t e = hipMemcpyAsync(d_dst + off, slot, n, hipMemcpyHostToDevice, c->h2d);
+        if (e == hipSuccess) e = hipEventRecord(c->ev_slot[s], c->h2d);
+        if (e != hipSuccess) {
+            *why = std::string("upload failed: ") + hipGetErrorString(e);
+            return false;
+        }
+        c->slot_used[s] = 1;
+    }
+    return true;
+}
+
+}  // namespace phd

@@ -17,6 +17,10 @@ pytestmark = pytest.mark.gpu
 
 FLOAT_RTOL = 1e-4          # north_star tolerance for float fields
 TIGHT_RTOL = 1e-9          # what fp64 actually delivers; tracked, not the contract
+# the compile-time column pass takes log(p) as e ln2 + fp32 log(mantissa)
+# (<= 2e-7 absolute per element, fft_ct.hip): bins of 12 MP images land within
+# ~4e-9 of the reference; tracked, not the contract
+BINS_TIGHT_RTOL = 1e-8
 
 CASES = golden_manifest()["cases"]
 
@@ -82,7 +86,7 @@ def test_report_matches_reference_fixture(case):
     # and the tighter bar fp64 actually reaches (reported separately for the record)
     st = rep.rgb_stats
     np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], g["stats"], rtol=TIGHT_RTOL)
-    np.testing.assert_allclose(np.array(rep.blur_profile.bins), g["bins"], rtol=TIGHT_RTOL, atol=1e-14)
+    np.testing.assert_allclose(np.array(rep.blur_profile.bins), g["bins"], rtol=BINS_TIGHT_RTOL, atol=1e-14)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])

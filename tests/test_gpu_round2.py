@@ -89,3 +89,22 @@ def test_batched_runtime_plan_with_downsample(shape):
         np.testing.assert_array_equal(np.array(r.color_palette.group_ids), o.valid_parents)
         np.testing.assert_array_equal(np.array(r.color_palette.quantities), o.palette_pct)
         np.testing.assert_allclose(_bins(r), o.bins, rtol=1e-4, atol=1e-12)
+
+
+def test_host_batch_pipelined_groups_match_device_reports():
+    """phd_report_batch_u8 with several same-size groups (16 + 4 + 3 images):
+    the uploads go through the pinned slot ring while the previous group
+    computes; every report equals the device-resident report of its image."""
+    phd, torch = _phd()
+    from photohive_dsp_amd import synth
+    imgs = [synth.make(("uniform", "structured", "hblur")[i % 3], 480, 640, 200 + i) for i in range(20)]
+    imgs += [synth.make("structured", 512, 512, 300 + i) for i in range(3)]
+    order = list(range(0, 23, 2)) + list(range(1, 23, 2))          # interleave the sizes
+    imgs = [imgs[i] for i in order]
+    reps = phd.get_reports(imgs)
+    for img, r in zip(imgs, reps):
+        one = phd.report_device(torch.from_numpy(img).cuda()[None].contiguous())[0]
+        assert r.color_palette.group_ids == one.color_palette.group_ids
+        assert r.color_palette.quantities == one.color_palette.quantities
+        assert np.array_equal(_bins(r), _bins(one))
+        assert [v.angle for v in r.blur_vectors] == [v.angle for v in one.blur_vectors]
