@@ -22,212 +22,13 @@
 // from a host-built table tw[t] = exp(-2 pi i t/n) (long-double accurate).
 #include <cstdlib>
 
-#include "phd_device.h"
+#include "fft_runtime.h"
 
 namespace phd {
 
+using namespace rt;
+
 namespace {
-
-__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
-    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ double2 mul_negi(double2 a) { return make_double2(a.y, -a.x); }   // a * (-i)
-__device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
-
-template <int R>
-__device__ __forceinline__ void butterfly(double2 (&v)[R]);
-
-template <>
-__device__ __forceinline__ void butterfly<2>(double2 (&v)[2]) {
-    const double2 a = v[0], b = v[1];
-    v[0] = cadd(a, b);
-    v[1] = csub(a, b);
-}
-
-template <>
-__device__ __forceinline__ void butterfly<3>(double2 (&v)[3]) {
-    constexpr double s1 = 0.86602540378443864676;   // sin(2 pi / 3)
-    const double2 t = cadd(v[1], v[2]);
-    const double2 d = mul_negi(cscale(csub(v[1], v[2]), s1));   // -i s1 (v1 - v2)
-    const double2 m = make_double2(v[0].x - 0.5 * t.x, v[0].y - 0.5 * t.y);
-    v[0] = cadd(v[0], t);
-    v[1] = cadd(m, d);
-    v[2] = csub(m, d);
-}
-
-template <>
-__device__ __forceinline__ void butterfly<4>(double2 (&v)[4]) {
-    const double2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
-    const double2 t2 = cadd(v[1], v[3]), t3 = mul_negi(csub(v[1], v[3]));
-    v[0] = cadd(t0, t2);
-    v[2] = csub(t0, t2);
-    v[1] = cadd(t1, t3);
-    v[3] = csub(t1, t3);
-}
-
-template <>
-__device__ __forceinline__ void butterfly<5>(double2 (&v)[5]) {
-    constexpr double c1 = 0.30901699437494742410;    // cos(2 pi / 5)
-    constexpr double c2 = -0.80901699437494742410;   // cos(4 pi / 5)
-    constexpr double s1 = 0.95105651629515357212;    // sin(2 pi / 5)
-    constexpr double s2 = 0.58778525229247312917;    // sin(4 pi / 5)
-    const double2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
-    const double2 t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
-    const double2 a1 = make_double2(v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y);
-    const double2 a2 = make_double2(v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y);
-    const double2 b1 = mul_negi(make_double2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y));
-    const double2 b2 = mul_negi(make_double2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y));
-    v[0] = cadd(v[0], cadd(t1, t2));
-    v[1] = cadd(a1, b1);
-    v[4] = csub(a1, b1);
-    v[2] = cadd(a2, b2);
-    v[3] = csub(a2, b2);
-}
-
-template <>
-__device__ __forceinline__ void butterfly<8>(double2 (&v)[8]) {
-    constexpr double h = 0.70710678118654752440;   // sqrt(1/2)
-    double2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
-    butterfly<4>(e);
-    butterfly<4>(o);
-    // o[k] *= W8^k
-    o[1] = make_double2(h * (o[1].x + o[1].y), h * (o[1].y - o[1].x));
-    o[2] = mul_negi(o[2]);
-    o[3] = make_double2(h * (o[3].y - o[3].x), -h * (o[3].x + o[3].y));
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        v[k] = cadd(e[k], o[k]);
-        v[k + 4] = csub(e[k], o[k]);
-    }
-}
-
-// a / d for 0 <= a < 2^23 through one float multiply and an exact correction
-// (the float quotient is off by at most one at these magnitudes).
-__device__ __forceinline__ int fdiv(int a, int d, float inv) {
-    int q = (int)((float)a * inv);
-    const int r = a - q * d;
-    q += (r >= d) ? 1 : 0;
-    q -= (r < 0) ? 1 : 0;
-    return q;
-}
-
-// W_n^e from the two LDS tables (e = 64*hi + lo).
-__device__ __forceinline__ double2 twiddle(const double2* lo, const double2* hi, int e) {
-    return cmul(hi[e >> 6], lo[e & 63]);
-}
-
-// One Stockham pass of radix R over `nseq` sequences of length n stored at
-// buf + seq*n (Govindaraju et al.: read stride n/R, write expanded index
-// (j/Ns)*Ns*R + j%Ns + r*Ns).  Every thread reads its butterflies' inputs to
-// registers, applies w^r (w = W_n^{(j%Ns)*n/(Ns*R)}, powers by multiplication),
-// runs the radix-R DFT, then -- after one barrier -- writes them back.
-// CAP = elements per block the kernel instance supports (8 per thread).
-template <int R, int T>
-__device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns, const double2* lo,
-                                           const double2* hi) {
-    constexpr int NB = (8 * T + R * T - 1) / (R * T);
-    const int nb = n / R, total = nb * nseq, tstep = n / (Ns * R);
-    const float inb = 1.0f / (float)nb, ins = 1.0f / (float)Ns;
-    double2 v[NB][R];
-    int dst[NB];
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-        const int t = threadIdx.x + b * T;
-        dst[b] = -1;
-        if (t < total) {
-            const int seq = nseq == 1 ? 0 : fdiv(t, nb, inb);
-            const int j = t - seq * nb;
-            const double2* s = buf + seq * n;
-#pragma unroll
-            for (int r = 0; r < R; r++) v[b][r] = s[j + r * nb];
-            const int jh = fdiv(j, Ns, ins), jm = j - jh * Ns;
-            if (jm != 0) {
-                const double2 w = twiddle(lo, hi, jm * tstep);
-                double2 wr = w;
-                v[b][1] = cmul(v[b][1], w);
-#pragma unroll
-                for (int r = 2; r < R; r++) {
-                    wr = cmul(wr, w);
-                    v[b][r] = cmul(v[b][r], wr);
-                }
-            }
-            butterfly<R>(v[b]);
-            dst[b] = seq * n + jh * Ns * R + jm;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-        if (dst[b] >= 0) {
-#pragma unroll
-            for (int r = 0; r < R; r++) buf[dst[b] + r * Ns] = v[b][r];
-        }
-    }
-    __syncthreads();
-}
-
-// Generic radix (any R, incl. a prime length itself): output-parallel direct DFT.
-template <int T>
-__device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns, int R,
-                                          const double2* __restrict__ tw) {
-    constexpr int EG = 8;   // outputs per thread (nseq*n <= 8*T)
-    const int nb = n / R, total = n * nseq, tstep = n / (Ns * R), nr = n / R;
-    double2 out[EG];
-    int dst[EG];
-#pragma unroll
-    for (int e = 0; e < EG; e++) {
-        const int t = threadIdx.x + e * T;
-        dst[e] = -1;
-        if (t < total) {
-            const int seq = t / n, rem = t - seq * n;
-            const int j = rem / R, k = rem - j * R;       // butterfly j, output k
-            const double2* s = buf + seq * n;
-            const int jm = j % Ns;
-            const int step = (jm * tstep + k * nr) % n;   // twiddle exponent per input r (mod n)
-            double2 acc = make_double2(0.0, 0.0);
-            int ex = 0;
-            for (int r = 0; r < R; r++) {
-                acc = cadd(acc, cmul(s[j + r * nb], tw[ex]));
-                ex += step;
-                if (ex >= n) ex -= n;
-            }
-            out[e] = acc;
-            dst[e] = seq * n + (j / Ns) * Ns * R + jm + k * Ns;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < EG; e++)
-        if (dst[e] >= 0) buf[dst[e]] = out[e];
-    __syncthreads();
-}
-
-template <int T, bool GEN>
-__device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan, const double2* lo, const double2* hi) {
-    int Ns = 1;
-    for (int p = 0; p < plan.npass; p++) {
-        const int R = plan.radix[p];
-        switch (R) {
-            case 2: stockham_pass<2, T>(buf, plan.n, nseq, Ns, lo, hi); break;
-            case 3: stockham_pass<3, T>(buf, plan.n, nseq, Ns, lo, hi); break;
-            case 4: stockham_pass<4, T>(buf, plan.n, nseq, Ns, lo, hi); break;
-            case 5: stockham_pass<5, T>(buf, plan.n, nseq, Ns, lo, hi); break;
-            case 8: stockham_pass<8, T>(buf, plan.n, nseq, Ns, lo, hi); break;
-            default:
-                if constexpr (GEN) generic_pass<T>(buf, plan.n, nseq, Ns, R, plan.tw);
-                break;
-        }
-        Ns *= R;
-    }
-}
-
-// Stage the two twiddle tables in LDS at `tw` (64 + n_hi entries).
-__device__ __forceinline__ void load_twiddles(double2* tw, const FftPlan& plan) {
-    for (int i = threadIdx.x; i < 64 + plan.n_hi; i += blockDim.x)
-        tw[i] = i < 64 ? plan.tw_lo[i] : plan.tw_hi[i - 64];
-}
 
 // LDS: [ W complex | twiddles (64 + n_hi) | k255 (256 doubles) ]
 template <int T, bool GEN>
