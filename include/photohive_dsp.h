@@ -211,6 +211,14 @@ int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int height, int widt
  * no compile-time FFT plan, or -1. */
 int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int width, double* d_out);
 
+/* Validation hook for the global-memory FFTs behind sides above 8192 px and
+ * lengths with a large prime factor (the reference's FFTW r2c takes any
+ * length, src/fft_processing.c:18-63): `count` contiguous complex sequences
+ * of length n (device, interleaved re/im) -> their unnormalised forward DFTs
+ * (e^{-i}) in d_out (d_out == d_in allowed).  Returns the plan kind (0 one
+ * LDS pass, 1 four-step, 2 Bluestein) or -1. */
+int phd_debug_gfft(const double* d_in, double* d_out, int n, long count);
+
 /* Free an Image_PGM returned by get_blur_profile_visual. */
 void phd_free_pgm(Image_PGM* img);
 

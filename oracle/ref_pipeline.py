@@ -205,8 +205,9 @@ class RefReport:
 
 
 def _image_rgb(img: np.ndarray):
-    """u8 HxWx3 -> reference Image_RGB of planar doubles k/255.0 (utils.py:30-46)."""
-    f = img.astype(np.float64) / 255.0
+    """u8 HxWx3 -> reference Image_RGB of planar doubles k/255.0 (utils.py:30-46);
+    a float64 HxWx3 image is passed as the doubles themselves (a C caller's)."""
+    f = img if img.dtype == np.float64 else img.astype(np.float64) / 255.0
     planes = [np.ascontiguousarray(f[..., c]).ravel() for c in range(3)]
     P = C.POINTER(C.c_double)
     im = Image_RGB(img.shape[0], img.shape[1], *[p.ctypes.data_as(P) for p in planes])
@@ -270,7 +271,7 @@ def blur_counts(h: int, wf: int, nr: int, na: int) -> np.ndarray:
 
 
 def report(img: np.ndarray, cfg: Config | None = None, crops=None, want_counts: bool = True) -> RefReport | None:
-    """The reference pipeline of src/interface.c:20-94 on a u8 image."""
+    """The reference pipeline of src/interface.c:20-94 on a u8 image (or float64 planes)."""
     cfg = cfg or Config()
     L = lib()
     im, _keep = _image_rgb(img)

@@ -233,6 +233,7 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
         return true;
     }
+    if (!gfft_direct_ok(width) || !gfft_direct_ok(height)) return select_generic(c, height, width, nbins, s);
     s->prow = get_plan(c, width);
     s->pcol = get_plan(c, height);
     if (!s->prow || !s->pcol) return false;
@@ -245,6 +246,7 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
                            const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st,
                            unsigned long long* rsum) {
+    if (s.generic) return generic_rows(s, img, nullptr, height, width, sums, nullptr, k255, inter, st);
     return s.ct ? launch_fft_rows_ct(img, height, width, sums, k255, s.tw_r, inter, st, rsum)
                 : launch_fft_rows(img, height, width, s.prow->plan, sums, k255, inter, st);
 }
@@ -256,6 +258,7 @@ hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, in
         return launch_fft_cols_ct(inter, height, width, wf, binmap, nbins, bin_sums, fmax_part, s.tw_c, sums, dbg,
                                   st);
     if (dbg) return hipErrorNotSupported;
+    if (s.generic) return generic_cols(s, const_cast<double2*>(inter), height, wf, binmap, nbins, bin_sums, fmax_part, st);
     return launch_fft_cols(inter, height, wf, s.pcol->plan, binmap, nbins, bin_sums, fmax_part, st);
 }
 

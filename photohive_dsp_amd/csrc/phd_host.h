@@ -82,6 +82,26 @@ struct FftPlanHost {
 };
 bool make_fft_plan(int n, FftPlanHost* p);
 
+// A batched 1-D transform of length n over sequences in HBM (fft_global.hip):
+// one LDS pass (direct), two (four-step n = n1 * n2) or Bluestein's
+// convolution through a smooth length M >= 2n - 1.
+struct GfftPlan {
+    enum { kDirect = 0, kFourStep = 1, kBluestein = 2 };
+    int n = 0, kind = kDirect;
+    const FftPlanHost* p = nullptr;                    // direct
+    const FftPlanHost *p1 = nullptr, *p2 = nullptr;    // four-step
+    double2* d_twn = nullptr;                          // four-step: W_n^e, e < n
+    int M = 0;                                         // Bluestein
+    const struct GfftPlan* sub = nullptr;
+    double2* d_chirp = nullptr;                        // c_j = exp(-pi i j^2 / n)
+    double2* d_bhat = nullptr;                         // FFT_M(conj c, wrapped)
+};
+// A length the LDS transforms take in one pass (n <= 8192, prime factors <= kMaxDirectPrime).
+bool gfft_direct_ok(int n);
+size_t gfft_scratch_elems(const GfftPlan& p, long count);
+// in -> out (in == out allowed), scratch of gfft_scratch_elems(p, count) elements
+bool gfft_run(const GfftPlan& p, const double2* in, double2* out, long count, double2* scr, hipStream_t st);
+
 // ---- per-kernel event timing (opt-in, phd_profile_kernels) -----------------
 enum KernelId { kK1 = 0, kFftRows = 1, kFftCols = 2, kCutoffs = 3, kPalSums = 4, kSharp = 5, kNumKernels = 6 };
 struct KernelProfiler {
@@ -130,6 +150,13 @@ struct Context {
     std::map<int, FftPlanHost> plans;
     std::map<std::pair<int, int>, double2*> ct_tw;  // (length, rows?) -> compile-time plan twiddles
     std::map<std::tuple<int, int, int, int>, BlurTable> tables;
+    std::map<int, GfftPlan> gplans;                 // global-memory FFT plans by length
+    double2* d_gbuf = nullptr;                      // generic 2-D path: row pairs + scratch
+    size_t gbuf_bytes = 0;
+    double* d_planes = nullptr;                     // planar input: r | g | b | luma (fp64)
+    size_t planes_bytes = 0;
+    void* d_prec = nullptr;                         // planar input: per-call records
+    size_t prec_bytes = 0;
     struct Cls {
         FastCls fc;
         ClassTables* d = nullptr;
@@ -202,6 +229,14 @@ struct FftSel {
     const double2* tw_r = nullptr;
     const double2* tw_c = nullptr;
     int col_blocks = 0;   // entries of the per-block max partials
+    // the generic path (a side above the LDS limit or with a large prime
+    // factor): row pairs -> global row transforms -> split / transpose, then
+    // the fused runtime column pass (cols_fused) or global column transforms
+    // + the power / binning pass
+    bool generic = false, cols_fused = false;
+    const GfftPlan* grow = nullptr;
+    const GfftPlan* gcol = nullptr;
+    double2* gbuf = nullptr;
 };
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s);
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
@@ -211,11 +246,36 @@ hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int 
 hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int width, int wf,
                            const uint16_t* binmap, int nbins, unsigned long long* bin_sums, double* fmax_part,
                            const unsigned long long* sums, double* dbg, hipStream_t st);
+const GfftPlan* get_gfft(Context* c, int n);
+bool select_generic(Context* c, int height, int width, int nbins, FftSel* s);
+// The generic path's row stage: luma from RGB8 (img, sums) or an fp64 plane
+// (pgm, avgd) into the column-major half spectrum `inter`.
+hipError_t generic_rows(const FftSel& s, const uint8_t* img, const double* pgm, int height, int width,
+                        const unsigned long long* sums, const double* avgd, const double* k255, double2* inter,
+                        hipStream_t st);
+hipError_t generic_cols(const FftSel& s, double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
+                        unsigned long long* bin_sums, double* fmax_part, hipStream_t st);
 const BlurTable* get_table(Context* c, int height, int width, int nr, int na);
 // Classification tables of a grid (uploaded once per configuration).
 const Context::Cls* get_cls(Context* c, const GridParams& gp);
 
 // ---- the pipeline -----------------------------------------------------------
+// pre_compute_error_checks (src/utilities.c:64-87) on the dimensions / crop boxes.
+bool precheck(int height, int width);
+bool check_crops(const Crop_Boundaries* cb, int height, int width);
+// pixels of the HSV image (downsample_rgb's size through `short`, src/image_processing.c:378-379)
+long hsv_count(int height, int width, int ds);
+// The Full_Report_Data tree (compile_full_report, src/utilities.c:210-226) from
+// the statistics, the palette decision and its slot sums pal[4k + {h, s, v, n}],
+// the polar bin sums (bin_scale fixed point) and spectrum max, the crop sums.
+Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const PaletteDecision& dec,
+                           const double* pal, long n_hsv, const BlurTable& tbl, const unsigned long long* bin_sums,
+                           double fmax, const phd_config& cfg, const Crop_Boundaries* crops,
+                           const double* sharp_sums, std::string* why);
+// get_full_report_data on the caller's planar doubles (phd_planar.cpp): the
+// RGB8 pipeline when every value is k/255.0, else the fp64 planar kernels.
+Full_Report_Data* report_planar(Context* c, const double* r, const double* g, const double* b, int height,
+                                int width, const phd_config& cfg, const Crop_Boundaries* crops);
 struct ImageIn {
     const uint8_t* d_img;   // device RGB8, rows of 3*width bytes
 };

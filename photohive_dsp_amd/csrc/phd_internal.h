@@ -29,6 +29,9 @@ constexpr int kThreads = 256;
 // Largest FFT length kept resident in LDS (complex fp64, 16 B/element).
 constexpr int kFftMaxLds = 8192;
 constexpr int kMaxFftPasses = 24;
+// Largest prime radix the LDS transforms take as an O(R) direct-DFT pass;
+// lengths with a larger prime factor go through Bluestein (fft_global.hip).
+constexpr int kMaxDirectPrime = 61;
 // Polar-bin sums of log(p) are accumulated as unsigned 64-bit fixed point
 // (value * bin_scale): integer additions commute, so the bins -- and the
 // strict threshold comparisons vectorize_blur_profile makes on them -- are the
@@ -283,6 +286,54 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,
                               int nbins, unsigned long long* bin_sums, double* fmax_part, const double2* tw,
                               const unsigned long long* sums, double* dbg, hipStream_t st);
+// Same, the luma from an fp64 plane when pgm != nullptr (planar input).
+hipError_t launch_sharpness_src(const uint8_t* img, const double* pgm, int height, int width, int n, const int* top,
+                                const int* bottom, const int* left, const int* right, const double* k255,
+                                double* sums, hipStream_t st);
+
+// ---- fp64 planar input of the legacy entry point (planar.hip) ---------------
+struct PlanarSrc {
+    const double* r;
+    const double* g;
+    const double* b;
+};
+constexpr int kPlanarBlocks = 1024;
+// flags: bit 0 not an 8-bit image, bit 1 non-finite value, bit 2 group index out of range
+hipError_t launch_planar_to_u8(const PlanarSrc& P, long n, uint8_t* rgb, int* flags, hipStream_t st);
+int planar_blocks(long n);   // partials of launch_planar_stats (per channel)
+// part1 / part2 [planar_blocks][3]: sums of x and of (x - mean)^2; *avg = (Br + Bg + Bb) / 3; pgm = luma plane
+hipError_t launch_planar_stats(const PlanarSrc& P, long n, double* pgm, double* part1, double* part2, double* avg,
+                               int* flags, hipStream_t st);
+hipError_t launch_planar_k1(const PlanarSrc& P, int height, int width, int ds, const GridParams& gp, unsigned* hist,
+                            unsigned short* chunk_hist, double* s_part, int* flags, hipStream_t st);
+hipError_t launch_planar_tail(const PlanarSrc& P, int height, int width, int ds, const GridParams& gp,
+                              const unsigned short* chunk_hist, int nchunks, GroupRule* rules, const int* search,
+                              int n_search, const double* off, int nslots, double* out, hipStream_t st);
+
+// ---- global-memory batched FFTs and the generic 2-D path (fft_global.hip) ----
+// Blocks of the generic path's power / binning pass (= its max partials).
+constexpr int kPowerBinBlocks = 1024;
+// `count` contiguous sequences of length plan.n <= 8192, in place allowed.
+hipError_t launch_gfft_direct(const double2* in, double2* out, long count, const FftPlan& plan, hipStream_t st);
+// n = p1.n * p2.n: in -> scr (n1-point transforms, twiddles twn[e] = W_n^e) -> out.
+hipError_t launch_gfft_4step(const double2* in, double2* out, double2* scr, long count, int n, const FftPlan& p1,
+                             const FftPlan& p2, const double2* twn, hipStream_t st);
+// Bluestein's pointwise steps (chirp c_j = exp(-pi i j^2 / n), bhat = FFT_M(conj c)).
+hipError_t launch_blu_pre(const double2* x, double2* a, int n, int M, long count, const double2* chirp,
+                          hipStream_t st);
+hipError_t launch_blu_mid(double2* a, long count, int M, const double2* bhat, hipStream_t st);
+hipError_t launch_blu_post(const double2* z, double2* out, int n, int M, long count, const double2* chirp,
+                           hipStream_t st);
+// Row pairs of the luma minus the DC bias: Z [ceil(H/2)][W] complex.  Luma from
+// RGB8 (img, k255) or an fp64 plane (pgm); avg from RGB8 sums or *avgd.
+hipError_t launch_pairs(const uint8_t* img, const double* pgm, int height, int width, const double* k255,
+                        const unsigned long long* sums, const double* avgd, double2* Z, hipStream_t st);
+// Row-pair spectra Z -> the column-major half spectrum inter [W/2+1][H].
+hipError_t launch_split_t(const double2* Z, int height, int width, double2* inter, hipStream_t st);
+// Power, max partials (kPowerBinBlocks) and polar log-binning of inter [wf][H].
+hipError_t launch_power_bins(const double2* X, int height, int wf, const uint16_t* binmap, int nbins,
+                             unsigned long long* bin_sums, double* fmax_part, hipStream_t st);
+
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st);
 hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st);

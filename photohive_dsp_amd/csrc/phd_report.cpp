@@ -78,6 +78,9 @@ Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolbl
     return L;
 }
 
+}  // namespace
+
+// shared with the planar path (phd_planar.cpp)
 bool check_crops(const Crop_Boundaries* cb, int height, int width) {
     if (!cb) return true;
     if (cb->N < 0 || (cb->N > 0 && (!cb->top || !cb->bottom || !cb->left || !cb->right))) {
@@ -221,6 +224,8 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
     return r;
 }
 
+namespace {
+
 RGB_Statistics stats_from_sums(const unsigned long long* m, long n) {
     // mean = sum(k)/255/N; population variance from exact integer moments:
     // var = (N*sum(k^2) - sum(k)^2) / (255^2 N^2)   (filtering.c:125-148 in exact arithmetic)
@@ -345,11 +350,6 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         return false;
     }
     if (!precheck(height, width) || !check_crops(crops, height, width)) return false;
-    if (width > kFftMaxLds || height > kFftMaxLds) {
-        set_error("image side above " + std::to_string(kFftMaxLds) +
-                  " px is not supported by this build's LDS-resident FFT");
-        return false;
-    }
     const hipStream_t st = work_stream(c, stream);
     while ((int)c->ev_img_fft.size() < n) {
         hipEvent_t a, b;
@@ -406,9 +406,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // (grid.y = image), the group's intermediates within 128 MB (half the
     // MALL); small images are otherwise bound by per-launch latency
     static const bool gbatch_off = getenv("PHD_FFT_NO_BATCH") != nullptr;
-    const bool gbatch = !fs.ct && !gbatch_off && n > 1 && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
+    const bool gbatch = !fs.ct && !fs.generic && !gbatch_off && n > 1 && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
     if (gbatch) Q = std::max(1, std::min(n, (int)(((size_t)128 << 20) / inter_one)));
-    const bool pipe = !gbatch && Q == 1 && n > 1 && pipe_env;
+    const bool pipe = !gbatch && !fs.generic && Q == 1 && n > 1 && pipe_env;
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)(pipe ? 2 : Q) * inter_one))
         return false;
@@ -902,22 +902,12 @@ extern "C" Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundar
                    blur_cutoff_ratio_denom};
     if (getenv("PHD_VERBOSE"))   // interface.c:34-35 prints this unconditionally
         printf("\n There are %d cores available to the C program.\n\n", (int)sysconf(_SC_NPROCESSORS_ONLN));
-    // planar doubles (utils.py:30-46 produces k/255.0) -> interleaved RGB8
-    const size_t n = (size_t)image->height * image->width;
-    std::vector<uint8_t> rgb(3 * n);
-    const Pixel* ch[3] = {image->r, image->g, image->b};
-    for (int c = 0; c < 3; c++)
-        for (size_t i = 0; i < n; i++) {
-            const double x = ch[c][i];
-            const long k = std::lround(x * 255.0);
-            if (k < 0 || k > 255 || (double)k / 255.0 != x) {
-                set_error("get_full_report_data: channel values must be k/255.0 for integer k in [0,255] "
-                          "(8-bit images); arbitrary doubles are not supported by the MI355X path");
-                return nullptr;
-            }
-            rgb[3 * i + c] = (uint8_t)k;
-        }
-    return report_from_host(rgb.data(), image->height, image->width, 0, &cfg, crops);
+    // planar doubles: the RGB8 pipeline when they are k/255.0 (utils.py:30-46),
+    // else the reference's fp64 arithmetic on them (phd_planar.cpp)
+    Context* c = get_context();
+    if (!c) return nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return report_planar(c, image->r, image->g, image->b, image->height, image->width, cfg, crops);
 }
 
 extern "C" void free_full_report(Full_Report_Data** report) {
@@ -1045,10 +1035,6 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
         return -1;
     }
     if (!precheck(height, width)) return -1;
-    if (width > kFftMaxLds || height > kFftMaxLds) {
-        set_error("image side above " + std::to_string(kFftMaxLds) + " px: the LDS-resident FFT rejects it");
-        return -1;
-    }
     Context* c = get_context();
     if (!c) return -1;
     std::lock_guard<std::mutex> lk(c->mu);

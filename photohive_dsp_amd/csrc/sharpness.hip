@@ -12,14 +12,17 @@ namespace phd {
 
 namespace {
 
-__device__ __forceinline__ double luma(const uint8_t* __restrict__ img, long i, const double* k255) {
+// the luma of pixel i: rgb2pgm of the RGB8 bytes, or the fp64 plane (planar input)
+__device__ __forceinline__ double luma(const uint8_t* __restrict__ img, const double* __restrict__ pgm, long i,
+                                       const double* k255) {
+    if (pgm) return pgm[i];
     return 0.299 * k255[img[3 * i]] + 0.587 * k255[img[3 * i + 1]] + 0.114 * k255[img[3 * i + 2]];
 }
 
 // f(y,x) of filter_image: sum over the 3x3 window in (fy, fx) order of
 // input * coef, skipping taps outside the crop.
-__device__ __forceinline__ double lap_at(const uint8_t* __restrict__ img, int width, int top, int left,
-                                         int ch, int cw, int y, int x, const double* k255) {
+__device__ __forceinline__ double lap_at(const uint8_t* __restrict__ img, const double* __restrict__ pgm, int width,
+                                         int top, int left, int ch, int cw, int y, int x, const double* k255) {
     double dp = 0.0;
 #pragma unroll
     for (int fy = 0; fy < 3; fy++)
@@ -28,13 +31,14 @@ __device__ __forceinline__ double lap_at(const uint8_t* __restrict__ img, int wi
             const int iy = y + fy - 1, ix = x + fx - 1;
             if (iy >= 0 && iy < ch && ix >= 0 && ix < cw) {
                 const double coef = (fy == 1 && fx == 1) ? 8.0 : -1.0;
-                dp += luma(img, (long)(iy + top) * width + ix + left, k255) * coef;
+                dp += luma(img, pgm, (long)(iy + top) * width + ix + left, k255) * coef;
             }
         }
     return dp;
 }
 
-__global__ __launch_bounds__(kThreads) void k_sharp_pass(const uint8_t* __restrict__ img, int width, int top,
+__global__ __launch_bounds__(kThreads) void k_sharp_pass(const uint8_t* __restrict__ img,
+                                                         const double* __restrict__ pgm, int width, int top,
                                                          int left, int ch, int cw,
                                                          const double* __restrict__ k255g,
                                                          const double* __restrict__ mean_src, long n_mean,
@@ -48,7 +52,7 @@ __global__ __launch_bounds__(kThreads) void k_sharp_pass(const uint8_t* __restri
     double acc = 0.0;
     for (long i = (long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long)gridDim.x * kThreads) {
         const int y = (int)(i / cw), x = (int)(i - (long)y * cw);
-        const double f = lap_at(img, width, top, left, ch, cw, y, x, k255);
+        const double f = lap_at(img, pgm, width, top, left, ch, cw, y, x, k255);
         if (mean_src) {
             const double d = f - mean;
             acc += d * d;
@@ -72,14 +76,20 @@ __global__ __launch_bounds__(kThreads) void k_sharp_pass(const uint8_t* __restri
 hipError_t launch_sharpness(const uint8_t* img, int height, int width, int n, const int* top,
                             const int* bottom, const int* left, const int* right, const double* k255,
                             double* sums, hipStream_t st) {
+    return launch_sharpness_src(img, nullptr, height, width, n, top, bottom, left, right, k255, sums, st);
+}
+
+hipError_t launch_sharpness_src(const uint8_t* img, const double* pgm, int height, int width, int n, const int* top,
+                                const int* bottom, const int* left, const int* right, const double* k255,
+                                double* sums, hipStream_t st) {
     (void)height;
     for (int k = 0; k < n; k++) {
         const int cw = right[k] - left[k], ch = bottom[k] - top[k];
         const long cn = (long)cw * ch;
         const int blocks = (int)std::min<long>(1024, (cn + kThreads - 1) / kThreads);
-        phd_launch(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, width, top[k], left[k],
+        phd_launch(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, pgm, width, top[k], left[k],
                            ch, cw, k255, (const double*)nullptr, 0L, sums + 2 * k);
-        phd_launch(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, width, top[k], left[k],
+        phd_launch(k_sharp_pass, dim3(blocks), dim3(kThreads), 0, st, img, pgm, width, top[k], left[k],
                            ch, cw, k255, (const double*)(sums + 2 * k), cn, sums + 2 * k + 1);
     }
     return hipGetLastError();

@@ -128,3 +128,13 @@ KINDS = {
 
 def make(kind: str, h: int, w: int, seed: int) -> np.ndarray:
     return KINDS[kind](h, w, seed)
+
+
+def deep(kind: str, h: int, w: int, seed: int) -> np.ndarray:
+    """A 16-bit image as the planar doubles a C caller of get_full_report_data
+    may pass (value / 65535, src/interface.c:20-94): the 8-bit `kind` image
+    scaled by 257 plus 8 bits of uniform noise.  float64 HxWx3 in [0, 1],
+    almost no value equal to any k/255.0."""
+    base = make(kind, h, w, seed).astype(np.float64) * 257.0
+    noise = uniform(h, w, seed + 7919).astype(np.float64)
+    return np.minimum(base + noise, 65535.0) / 65535.0

@@ -33,9 +33,19 @@ def golden_case(name):
         return {k: z[k] for k in z.files}
 
 
+BIG_PIXELS = 50_000_000          # the 120 MP fixtures: generated once per session
+_big_images = {}
+
+
 def golden_image(case):
     from photohive_dsp_amd import synth
-    return synth.make(case["kind"], case["height"], case["width"], case["seed"])
+    key = (case["kind"], case["height"], case["width"], case["seed"])
+    if key in _big_images:
+        return _big_images[key]
+    img = synth.make(*key)
+    if case["height"] * case["width"] >= BIG_PIXELS:
+        _big_images[key] = img
+    return img
 
 
 @pytest.fixture(scope="session")

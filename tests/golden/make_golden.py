@@ -55,6 +55,25 @@ CASES = [
     ("structured_640x480_hsv36", "structured", 640, 480, 22, HSV36, None),
     ("dominant_1280x720_hsv36", "dominant", 1280, 720, 23, HSV36, None),
     ("structured_3000x4000_hsv36", "structured", 3000, 4000, 24, HSV36, None),
+    # sides above the 8192-point LDS transforms and lengths with large prime
+    # factors: the reference takes up to 120 MP in 1:5..5:1 (src/utilities.c:12,
+    # 73-80) and FFTW any length (src/fft_processing.c:18-63)
+    ("uniform_10000x12000", "uniform", 10000, 12000, 31, {}, None),          # four-step rows and columns
+    ("structured_12000x10000", "structured", 12000, 10000, 32, {}, None),
+    ("hblur_1700x8209_prime", "hblur", 1700, 8209, 33, {}, None),            # Bluestein rows (8209 prime)
+    ("motion_9000x2000", "motion", 9000, 2000, 34, {}, None),                # four-step columns only
+    ("structured_1201x1009_primes", "structured", 1201, 1009, 35, HSV36, None),  # Bluestein both ways, odd H
+]
+
+# get_full_report_data on planar doubles that are not k/255 (a C caller's
+# 16-bit image / 65535, synth.deep): name, kind, H, W, seed, config, crops
+PLANAR_CASES = [
+    ("deep_structured_600x800_crops", "structured", 600, 800, 41, {},
+     [dict(top=10, bottom=210, left=20, right=320), dict(top=300, bottom=599, left=400, right=799)]),
+    ("deep_uniform_700x900_ds2_L50", "uniform", 700, 900, 42, {"downsample_rate": 2, "linked_list_size": 50}, None),
+    ("deep_motion_1201x1009_hsv36", "motion", 1201, 1009, 43, HSV36, None),
+    ("deep_dominant_1024x1536", "dominant", 1024, 1536, 44, {}, None),
+    ("deep_hblur_3000x4000", "hblur", 3000, 4000, 45, {}, None),
 ]
 
 # get_blur_profile_visual (src/blur_profile.c:140-180) on a Blur_Profile whose
@@ -94,7 +113,8 @@ def main(argv=None):
     old = {}
     if only is not None and os.path.exists(path):
         with open(path) as f:
-            old = {c["name"]: c for c in json.load(f)["cases"]}
+            m0 = json.load(f)
+            old = {c["name"]: c for c in m0["cases"] + m0.get("planar_cases", [])}
     manifest = {"cases": [], "errors": []}
     for name, kind, h, w, seed, kw, crops in CASES:
         entry = dict(name=name, kind=kind, height=h, width=w, seed=seed, config=kw, crops=crops)
@@ -110,6 +130,24 @@ def main(argv=None):
                       blur_angles=r.blur_angles, blur_mags=r.blur_mags, fft_max=np.array(r.fft_max),
                       angle_bin_size=np.array(r.angle_bin_size),
                       radius_bin_size=np.array(r.radius_bin_size),
+                      image_sha=np.frombuffer(__import__("hashlib").sha256(img.tobytes()).digest(),
+                                              dtype=np.uint8))
+        if r.sharpness is not None:
+            arrays["sharpness"] = r.sharpness
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+        print("wrote", name, flush=True)
+    for name, kind, h, w, seed, kw, crops in PLANAR_CASES:
+        entry = dict(name=name, kind=kind, height=h, width=w, seed=seed, config=kw, crops=crops)
+        manifest.setdefault("planar_cases", []).append(entry)
+        if only is not None and name not in only:
+            assert name in old or os.path.exists(os.path.join(HERE, f"{name}.npz")), f"{name} has no fixture yet"
+            continue
+        img = synth.deep(kind, h, w, seed)
+        r = rp.report(img, rp.Config(**kw), crops=crops)
+        arrays = dict(stats=r.stats, average_saturation=np.array(r.average_saturation), hist=r.hist,
+                      valid_parents=r.valid_parents, kept=r.kept, palette_hsv=r.palette_hsv,
+                      palette_pct=r.palette_pct, bins=r.bins, blur_angles=r.blur_angles, blur_mags=r.blur_mags,
+                      angle_bin_size=np.array(r.angle_bin_size), radius_bin_size=np.array(r.radius_bin_size),
                       image_sha=np.frombuffer(__import__("hashlib").sha256(img.tobytes()).digest(),
                                               dtype=np.uint8))
         if r.sharpness is not None:
