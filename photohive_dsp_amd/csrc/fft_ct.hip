@@ -247,7 +247,7 @@ struct ColK {
     // waves per SIMD of the launch bounds: one-column blocks are sized for two
     // resident blocks per CU, one when the column and twiddles fill the LDS
     static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
-    static constexpr int MINW = NC == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2 : 1;
+    static constexpr int MINW = (CPB & 16) ? (3 * ((T + 63) / 64) + 3) / 4 : (NC == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2 : 1);
     static_assert(NC == 1 || NC == 2, "columns per block");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
 };

@@ -27,8 +27,9 @@
 //     n255) / 255 + 0.999999 n255 all follow from it; h and s are two fp64 LDS
 //     atomics (h = N * (1/kd), s = kd * (1/kmax) or rgb2hsv's 0.999999, the
 //     reciprocals from an LDS table).
-// A non-special hue exactly on a half-bin boundary (rare) is resolved after
-// the chunk in fp64 with palette.hip's fused_exact, as before.
+// A non-special hue exactly on a half-bin boundary (rare) is counted after the
+// chunk's classification by its own thread in fp64 (t_exact, palette.hip's
+// fused_exact decisions).
 //
 // One block of 1024 threads per CU (the table takes 64 KiB of LDS); each
 // block walks a contiguous run of (image, 16384-pixel chunk) items, 16 pixels
@@ -37,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "phd_device.h"
 
@@ -44,9 +46,12 @@ namespace phd {
 
 namespace {
 
-constexpr int kT = 1024;                                  // threads per block
+#ifndef PHD_K1_T
+#define PHD_K1_T 1024
+#endif
+constexpr int kT = PHD_K1_T;                              // threads per block
 constexpr int kG = kChunk / (4 * kT);                     // 4-pixel groups per thread per chunk
-static_assert(kG == 4, "K1 tile");
+static_assert(kG == 4 || kG == 8, "K1 tile");
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) unsigned gu32t;
@@ -58,9 +63,8 @@ __device__ __forceinline__ unsigned as1(u16x2 x) { return __builtin_bit_cast(uns
 // reciprocals, the code tables) lies below 64 KiB, so it is a DS
 // instruction's immediate offset (no address add per access); the per-run
 // records and the queue follow the 64 KiB code table.
-constexpr int kQueue = 2048;                              // deferred-pixel queue (chunk offsets, u32)
 struct TVar {
-    int cells, gs2, ce, inv, k255, red, code, rcell, cg, seg, r255, rmx, dq, qcnt, end;
+    int cells, gs2, ce, inv, k255, red, code, rcell, cg, seg, r255, rmx, end;
 };
 __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     const int C = 1 << cshift;
@@ -77,15 +81,29 @@ __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     v.seg = v.cg + 4 * tl;                                          // tl u32
     v.r255 = v.seg + 4 * tl;                                        // tl u32
     v.rmx = (v.r255 + 4 * tl + 7) & ~7;                             // tl u64
-    v.dq = v.rmx + 8 * tl;                                          // kQueue u32
-    v.qcnt = v.dq + 4 * kQueue;                                     // u32 (+ pad)
-    v.end = v.qcnt + 16;
+    v.end = v.rmx + 8 * tl;
     return v;
 }
 
 struct TConst {
     int lh, hp, spvp, ac, tl, gs, cgs, hp2, ncell, cshift, mycopy;
 };
+
+__host__ __device__ inline TConst make_tconst(const GridParams& gp, int cshift, int mycopy) {
+    TConst X;
+    X.lh = (360 / gp.hp) & 0xFFFF;                            // 16 bits: v_mul_u32_u24
+    X.hp = gp.hp;
+    X.spvp = gp.sp * gp.vp;
+    X.ac = 4 * X.spvp - 2;
+    X.tl = gp.tl;
+    X.gs = gp.tl - gp.ng - 1;
+    X.cgs = 4 * X.gs;
+    X.hp2 = 2 * gp.hp;
+    X.ncell = HueCells::count(gp);
+    X.cshift = cshift;
+    X.mycopy = mycopy;
+    return X;
+}
 
 // The group of hue cell q (HueCells layout).
 __device__ __forceinline__ int group_of_cell(int q, const TConst& X) {
@@ -192,6 +210,12 @@ __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k2
     atomicAdd(a + 1, s);
 }
 
+// byte k (< 12) of a 4-pixel group's three words
+__device__ __forceinline__ int group_byte(unsigned a0, unsigned a1, unsigned a2, int k) {
+    const unsigned w = k < 4 ? a0 : (k < 8 ? a1 : a2);
+    return (int)((w >> (8 * (k & 3))) & 255u);
+}
+
 struct Mom {
     unsigned sr, sg, sb, qr, qg, qb;
 };
@@ -257,18 +281,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                     // block-uniform
     const int C = 1 << cshift, cm = C - 1;
-    TConst X;
-    X.lh = (360 / gp.hp) & 0xFFFF;                            // 16 bits: v_mul_u32_u24
-    X.hp = gp.hp;
-    X.spvp = gp.sp * gp.vp;
-    X.ac = 4 * X.spvp - 2;
-    X.tl = gp.tl;
-    X.gs = gp.tl - gp.ng - 1;
-    X.cgs = 4 * X.gs;
-    X.hp2 = 2 * gp.hp;
-    X.ncell = HueCells::count(gp);
-    X.cshift = cshift;
-    X.mycopy = tid & cm;
+    const TConst X = make_tconst(gp, cshift, tid & cm);
     const TVar V = t_var(X.tl, X.ncell, cshift);
     unsigned char* code8 = smem + V.code;
     double* inv = reinterpret_cast<double*>(smem + V.inv);
@@ -280,9 +293,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
     unsigned* seg = reinterpret_cast<unsigned*>(smem + V.seg);
     unsigned* r255 = reinterpret_cast<unsigned*>(smem + V.r255);
     unsigned long long* rmx = reinterpret_cast<unsigned long long*>(smem + V.rmx);
-    unsigned* dq = reinterpret_cast<unsigned*>(smem + V.dq);
     double* k255 = reinterpret_cast<double*>(smem + V.k255);
-    unsigned* qcnt = reinterpret_cast<unsigned*>(smem + V.qcnt);
     {
         const uint4* src = reinterpret_cast<const uint4*>(tabs->code8);
         uint4* dst = reinterpret_cast<uint4*>(code8);
@@ -363,35 +374,28 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
                     t_exact(kr, kg, kb, k255, gp, code8, inv, cells, gs2, X);
             }
         }
-        // deferred pixels: queued in LDS (chunk offsets) and resolved by all
-        // threads together after the barrier, so a wave does not idle while a
-        // few of its lanes run the fp64 path; past the queue's capacity in place
-        if (emask) {
-            int pos = (int)atomicAdd(qcnt, (unsigned)__popc(emask));
-            while (emask) {
-                const int bt = __ffs(emask) - 1;
-                emask &= emask - 1;
-                const int off = 4 * tid + 4 * kT * (bt >> 2) + (bt & 3);
-                if (pos < kQueue) {
-                    dq[pos++] = (unsigned)off;
-                } else {
-                    const long p = base + off;
-                    t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp, code8, inv, cells, gs2, X);
+        // deferred pixels (a hue exactly on a half-bin boundary, ~1.7 % of uniform
+        // pixels): the thread counts its own in fp64 from the chunk words it still
+        // holds (no LDS queue, no extra barrier; measured the same time as the
+        // queue resolved by the whole block, and as a 4 MiB decision table)
+        while (emask) {
+            const int bt = __ffs(emask) - 1;
+            emask &= emask - 1;
+            const int gst = bt >> 2, pi = bt & 3;
+            unsigned a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+            for (int st = 0; st < kG; st++)
+                if (st == gst) {
+                    a0 = cw[st][0];
+                    a1 = cw[st][1];
+                    a2 = cw[st][2];
                 }
-            }
+            t_exact(group_byte(a0, a1, a2, 3 * pi), group_byte(a0, a1, a2, 3 * pi + 1),
+                    group_byte(a0, a1, a2, 3 * pi + 2), k255, gp, code8, inv, cells, gs2, X);
         }
         const long pad = base + kChunk - full_end;                // zero pixels of masked groups
         if (pad > 0 && tid == 0) atomicAdd(&cells[zcell << cshift], (unsigned long long)(-pad));
         __syncthreads();
-        const int nq = min((int)*qcnt, kQueue);                   // block-uniform
-        if (nq > 0) {
-            for (int i = tid; i < nq; i += kT) {
-                const long p = base + dq[i];
-                t_exact(cip[3 * p], cip[3 * p + 1], cip[3 * p + 2], k255, gp, code8, inv, cells, gs2, X);
-            }
-            __syncthreads();
-        }
-        if (tid == 0) *qcnt = 0u;                                 // read by all before the fold's barrier
         // fold the chunk's cells: one thread per cell sums its C copies (consecutive
         // u64); the run's cell counts, per-group sum(kmax) / n255 and the chunk's group counts
         for (int q = tid; q < ((abl & 8) ? 0 : X.ncell + 1); q += kT) {
@@ -498,8 +502,9 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
 int k1t_cshift(const GridParams& gp, const ClassTables& t) {
     if (!t.codes_ok) return -1;
     const int ncell = HueCells::count(gp);
+    static const int budget = getenv("PHD_K1_LDS_KB") ? atoi(getenv("PHD_K1_LDS_KB")) : 158;
     for (int cs = 4; cs >= 0; cs--)
-        if (t_var(gp.tl, ncell, cs).end <= 158 * 1024) return cs;
+        if (t_var(gp.tl, ncell, cs).end <= budget * 1024) return cs;
     return -1;
 }
 
@@ -516,8 +521,9 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     }
     const int grid = (int)std::min<long>(nitems, (long)num_cus());
     phd_launch(k_k1t, dim3(grid), dim3(kT), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255, out0,
-                       a_stride, h_stride, cshift, env_ablate());
+                       a_stride, h_stride, cshift, g_ablate | env_ablate());
     return hipGetLastError();
 }
 
 }  // namespace phd
+
