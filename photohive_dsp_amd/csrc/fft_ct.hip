@@ -23,17 +23,20 @@
 // separated, A[k] = (Z[k] + conj Z[W-k]) / 2 and B[k] = (Z[k] - conj Z[W-k]) / 2i,
 // and stored as the pair's contiguous tile row.
 //
-// Column kernel (persistent, one block of 2 x T threads per CU, a contiguous
-// range of column pairs per block; each half of the block transforms one
-// column of the pair).  The next column pair is prefetched into registers.
-// The last pass's outputs never go back to LDS: the epilogue forms p = re^2 +
-// im^2, keeps the block's max and writes log(p) (p >= 1) per spectrum row to
-// LDS; each thread then sums a contiguous run of rows, one LDS atomic per
-// run of one polar bin.  The block adds its non-zero bins to the image's bin
-// sums at the end.
+// Column kernel (persistent, two blocks of T threads per CU, one column at a
+// time per block; blocks b, b^8, b^16, b^24 of one XCD take the four columns
+// of the same 128-byte lines, each block a contiguous range of line pairs).
+// The next column is prefetched into registers.
+// The last pass's outputs never go back to LDS as spectra: the epilogue forms
+// p = re^2 + im^2, keeps the block's max and writes p (1 for p < 1, whose log
+// the reference clamps away) per spectrum row to LDS; each thread then walks a
+// contiguous run of rows and adds one LDS atomic per run of one polar bin.  The
+// block adds its non-zero bins to the image's bin sums at the end.
 //
-// log(p) for the bins: p = m * 2^e (frexp), log p = e ln2 + log(m) with log(m)
-// in fp32.  The absolute error is <= 2e-7 per element, against bin averages of
+// log(p) for the bins: a run's sum of log p is the log of its product.  The
+// frexp mantissas (in [1/2, 1)) multiply in fp64 and the exponents add, and
+// one fp32 log of the mantissa product closes the run: e ln2 + log(m).  The
+// absolute error is <= 2e-7 per run (~10 elements), against bin averages of
 // order 10 (north_star tolerance: 1e-4 relative).  The max and the p >= 1 test
 // stay in fp64.
 #include <cstdlib>
@@ -219,13 +222,6 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     }
 }
 
-// log(p) for p >= 1: e ln2 + log(m) with m = frexp mantissa and log(m) in fp32
-__device__ __forceinline__ double log_p(double p) {
-    int e;
-    const double m = frexp(p, &e);
-    return (double)e * 0.69314718055994530942 + (double)__logf((float)m);
-}
-
 template <int H, int T, int CPB, int... Rs>
 struct ColK {
     using PL = Plan<H, T, 1, Rs...>;
@@ -276,7 +272,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     const int tid = threadIdx.x;
     // NC == 1: blocks b, b^8, b^16, b^24 (one XCD) take the four columns of a
     // 128-byte line (two tiles), so each line is fetched once into that L2
-    const int quad = NC == 2 ? 0 : (int)((blockIdx.x >> 3) & 3);
+    // NC == 2: blocks b, b^8 (one XCD) take the two tiles of a 128-byte line
+    const int quad = NC == 2 ? (int)((blockIdx.x >> 3) & 1) * 2 : (int)((blockIdx.x >> 3) & 3);
     const int half = NC == 2 ? (tid >= T ? 1 : 0) : (quad & 1);   // column of the pair
     const int ht = NC == 2 ? tid - half * T : tid;
     double2* buf = bufs + (NC == 2 ? half * H : 0);
@@ -285,13 +282,14 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         for (int i = tid; i < nbins; i += NT) lb[i] = 0ull;
     unsigned long long* const bsum = K::GB ? bin_sums : lb;   // where the runs are added
     const int kpn = (wf + 1) / 2;
-    const int nunit = NC == 2 ? kpn : (kpn + 1) / 2;          // column pairs / tile pairs
-    const int nlog = NC == 2 ? (int)gridDim.x : (int)gridDim.x / 4;
-    const int lblk = NC == 2 ? (int)blockIdx.x : (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
+    const int nunit = (kpn + 1) / 2;                          // tile pairs (128-byte lines)
+    const int nlog = NC == 2 ? (int)gridDim.x / 2 : (int)gridDim.x / 4;
+    const int lblk = NC == 2 ? (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7))
+                             : (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
     const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
     // the column pair of step u (NC == 1: tile 2u or 2u+1; past the last tile
     // the block re-reads the last one and idles)
-    auto pair_at = [&](int u) { return NC == 2 ? u : min(2 * u + (quad >> 1), kpn - 1); };
+    auto pair_at = [&](int u) { return min(2 * u + (quad >> 1), kpn - 1); };
     // the tiles: element 4p + 2c + r is (row 2p + r, column 2kp + c).  NC == 2
     // loads whole 64-B tiles (thread -> row pair tid/4, sub-element tid%4), CPB
     // == 1 its column's 32-B half (row pair tid/2, row tid%2)
@@ -326,7 +324,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     dst[c * 2 * (NT / PER)] = pf[c];
             }
         }
-        const int col = NC == 2 ? 2 * kp + half : 2 * (2 * u + (quad >> 1)) + half;
+        const int col = 2 * (2 * u + (quad >> 1)) + half;
         const bool live = col < wf;                       // the phantom column of an odd wf idles
         // bin ids of this thread's run of its column: u in [ht*E, ht*E + E).  The
         // table has 64 bytes of padding, so the last run may read past its end.
@@ -367,7 +365,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
             L::compute(v, tw + K::PL::last_tw_offset, ht);
         }
         __syncthreads();                       // every thread has read its last-pass inputs
-        double* lgb = reinterpret_cast<double*>(buf);   // log p per spectrum row, -1 for p < 1
+        double* lgb = reinterpret_cast<double*>(buf);   // p per spectrum row, 1 for p < 1 (log 0)
 #pragma unroll
         for (int q = 0; q < L::ROUNDS; q++) {
             const int b = ht + q * T;
@@ -378,34 +376,41 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     const double p = X.x * X.x + X.y * X.y;          // src/fft_processing.c:49
                     if (live) mx = fmax(mx, p);
                     if (dbg && live) dbg[(size_t)col * H + b + k * L::NB] = p;
-                    lgb[b + k * L::NB] = (live && p >= 1) ? log_p(p) : -1.0;   // src/fft_processing.c:197-198
+                    lgb[b + k * L::NB] = (live && p >= 1) ? p : 1.0;   // src/fft_processing.c:197-198
                 }
             }
         }
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column), in bin_scale fixed point so that the
-        // sums do not depend on the order of the atomics
+        // sums do not depend on the order of the atomics.  A run's sum of log p
+        // is log of the product: the frexp mantissas multiply (>= 2^-E, no
+        // underflow), the exponents add, one fp32 log of the mantissa product per run.
         if (!(ablate & 2)) {
-            int cur = -1;
-            double acc = 0.0;
+            int cur = -1, esum = 0;
+            double mprod = 1.0;
+            auto flush = [&]() {
+                const double acc = fmax((double)esum * 0.69314718055994530942 + (double)__logf((float)mprod), 0.0);
+                atomicAdd(&bsum[cur], bin_fixed(acc, bscale));
+            };
 #pragma unroll
             for (int j = 0; j < K::E; j++) {
                 const int u = ht * K::E + j;
                 if ((H % K::E == 0 && K::E * T == H) || u < H) {
-                    const double lg = lgb[u];
-                    if (lg >= 0.0) {
-                        const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
-                        if (bin != cur) {
-                            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc, bscale));
-                            cur = bin;
-                            acc = 0.0;
-                        }
-                        acc += lg;
+                    const double pv = lgb[u];
+                    const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
+                    if (bin != cur) {
+                        if (cur >= 0) flush();
+                        cur = bin;
+                        mprod = 1.0;
+                        esum = 0;
                     }
+                    int e;
+                    mprod *= frexp(pv, &e);
+                    esum += e;
                 }
             }
-            if (cur >= 0) atomicAdd(&bsum[cur], bin_fixed(acc, bscale));
+            if (cur >= 0) flush();
         }
         __syncthreads();
     }
@@ -455,10 +460,12 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
 }
 
 template <int H, int T, int CPB, int... Rs>
-int cols_grid(int wf, int nbins) {
+int cols_grid(int, int nbins) {
     int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
-    const int kpn = (wf + 1) / 2;
-    if ((CPB & 3) == 2) return kpn < g ? kpn : g;
+    if ((CPB & 3) == 2) {
+        g = g / 16 * 16;                                    // XCD pairs b, b^8
+        return g < 16 ? 16 : g;
+    }
     g = g / 32 * 32;                                        // XCD quads b, b^8, b^16, b^24
     return g < 32 ? 32 : g;
 }

@@ -264,6 +264,9 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 3, 256, 5, 25, 12, 10)     \
     X(3000, 4, 512, 5, 5, 6, 10, 10)   \
     X(3000, 5, 300, 5, 5, 6, 10, 10)   \
+    X(3000, 6, 256, 2, 15, 10, 20)     \
+    X(3000, 7, 256, 6, 15, 10, 20)     \
+    X(3000, 8, 192, 2, 15, 10, 20)     \
     X(6000, 0, 512, 5, 15, 20, 20)     \
     X(6000, 1, 512, 5, 10, 20, 30)     \
     X(4000, 0, 320, 5, 10, 20, 20)     \
