@@ -232,9 +232,14 @@ struct ColK {
     // CPB = flags: bits 0-1 columns per block (1 or 2); 4: no register
     // prefetch (the step's tiles are loaded at its start, other blocks of the
     // CU hide the latency); 8: bins summed with global atomics (no LDS bins)
+    // 32: pass 0 from registers (one column per block: thread b < H/R0 loads
+    // rows b + r H/R0 of the next column, runs its first butterfly on them and
+    // stores the outputs -- no LDS round trip for the raw column)
     static constexpr int NC = CPB & 3;
     static constexpr bool PF = !(CPB & 4);
     static constexpr bool GB = (CPB & 8) != 0;
+    static constexpr bool P0R = (CPB & 32) != 0;
+    using PE = Peel<H, T, Rs...>;
     static constexpr int NT = NC * T;                                     // block size
     static constexpr int CR = (2 * NC * P + NT - 1) / NT;                 // load rounds
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
@@ -245,6 +250,7 @@ struct ColK {
     static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
     static constexpr int MINW = (CPB & 16) ? (3 * ((T + 63) / 64) + 3) / 4 : (NC == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2 : 1);
     static_assert(NC == 1 || NC == 2, "columns per block");
+    static_assert(!P0R || (NC == 1 && PF && PE::NB <= T && Radices<Rs...>::count >= 2), "pass 0 from registers");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
 };
 
@@ -308,13 +314,39 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
             pf[c] = src_[(size_t)pr_ * kpn * 4];                                            \
         }                                                                                   \
     } while (0)
-    if (K::PF && c0 < c1) PHD_COL_FETCH(pair_at(c0));
+    // K::P0R: thread ht < NB0 holds rows ht + r NB0 of its column (pass 0's inputs)
+    constexpr int R0 = K::PE::R, NB0 = K::PE::NB;
+    double2 p0v[1][K::P0R ? R0 : 1];
+    auto fetch0 = [&](int kpv) {
+        const double2* src = inter + ((size_t)kpv * 2 + half) * 2;
+        if (ht < NB0) {
+#pragma unroll
+            for (int r = 0; r < (K::P0R ? R0 : 1); r++) {
+                const int y = ht + r * NB0;
+                p0v[0][r] = src[(size_t)(y >> 1) * kpn * 4 + (y & 1)];
+            }
+        }
+    };
+    if (K::P0R && c0 < c1) fetch0(pair_at(c0));
+    else if (K::PF && c0 < c1) PHD_COL_FETCH(pair_at(c0));
     double mx = 0.0;
     __syncthreads();
     for (int u = c0; u < c1; u++) {
         const int kp = pair_at(u);
         if (!K::PF) PHD_COL_FETCH(kp);
-        {
+        if constexpr (K::P0R) {
+            if (kp == 0 && 2 * (2 * u + (quad >> 1)) + half == 0 && ht < NB0) {   // block-uniform kp, col
+                // remove_dc_bias on the registers (see below)
+                const double n = (double)H * (double)width;
+                const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
+                                    (double)sums[2] / 255.0 / n) / 3.0;
+                const double dc = (double)width * avg;
+#pragma unroll
+                for (int r = 0; r < R0; r++) p0v[0][r].x -= dc;
+            }
+            if (!(ablate & 1)) K::PE::P0::compute(p0v, tw, ht);
+            K::PE::P0::store(buf, p0v, ht);
+        } else {
             u32x4* dst = reinterpret_cast<u32x4*>(bufs + (NC == 2 ? ((psub >> 1) & 1) * H : 0) + 2 * prow0 +
                                                   (psub & 1));
 #pragma unroll
@@ -343,9 +375,9 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     bmw[j] = (unsigned)bcol[2 * j] | ((unsigned)bcol[2 * j + 1] << 16);
             }
         }
-        if (K::PF && u + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(pair_at(u + 1));
+        if (!K::P0R && K::PF && u + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(pair_at(u + 1));
         __syncthreads();
-        if (kp == 0) {                                    // block-uniform
+        if (!K::P0R && kp == 0) {                         // block-uniform
             // remove_dc_bias (src/blur_profile.c:233-238): a constant per image only
             // moves the row spectra's k = 0 column, by W * avg per row, with avg =
             // (Br + Bg + Bb) / 3 (src/interface.c:78) from K1's exact channel sums
@@ -358,7 +390,11 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
             }
             __syncthreads();
         }
-        if (!(ablate & 1)) K::PL::all_but_last(buf, tw, ht);
+        if constexpr (K::P0R) {
+            if (!(ablate & 1)) K::PE::RestPlan::all_but_last(buf, tw, ht);
+        } else {
+            if (!(ablate & 1)) K::PL::all_but_last(buf, tw, ht);
+        }
         double2 v[L::ROUNDS][R];
         if (!(ablate & 16)) {
             L::load(buf, v, ht);
@@ -380,6 +416,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                 }
             }
         }
+        // the next column's pass-0 inputs (p0v is free from here to the next step)
+        if (K::P0R && u + 1 < c1 && !(ablate & 4)) fetch0(pair_at(u + 1));
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column), in bin_scale fixed point so that the

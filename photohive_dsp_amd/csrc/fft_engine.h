@@ -277,5 +277,15 @@ struct Plan<N, T, NS, R> {
     __device__ static __forceinline__ void all_but_last(double2*, const double2*, int) {}
 };
 
+// The first pass peeled off a plan (a caller that holds pass 0's inputs in
+// registers runs P0 itself, then Rest::all_but_last from pass 1).
+template <int N, int T, int R0, int... Rest>
+struct Peel {
+    static constexpr int R = R0;
+    static constexpr int NB = N / R0;
+    using P0 = Pass<N, T, R0, 1>;
+    using RestPlan = Plan<N, T, R0, Rest...>;
+};
+
 }  // namespace fe
 }  // namespace phd
