@@ -64,7 +64,7 @@ __device__ __forceinline__ unsigned as1(u16x2 x) { return __builtin_bit_cast(uns
 // instruction's immediate offset (no address add per access); the per-run
 // records and the queue follow the 64 KiB code table.
 struct TVar {
-    int cells, gs2, ce, inv, k255, red, code, rcell, cg, seg, r255, rmx, end;
+    int cells, gs2, ce, inv, sinv, k255, red, code, rcell, cg, seg, r255, rmx, end;
 };
 __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     const int C = 1 << cshift;
@@ -72,8 +72,9 @@ __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     v.cells = 0;                                                    // (ncell+1) * C u64
     v.gs2 = v.cells + 8 * (ncell + 1) * C;                          // (tl+1) * C * {h, s} f64
     v.ce = v.gs2 + 16 * (tl + 1) * C;                               // 256 u32
-    v.inv = v.ce + 1024;                                            // 256 f64
-    v.k255 = v.inv + 2048;                                          // 256 f64: k / 255.0 (the exact path)
+    v.inv = v.ce + 1024;                                            // 256 f64: 0.5 / k (h = 2N * (0.5 / kd))
+    v.sinv = v.inv + 2048;                                          // 512 f64: s = kd * sinv[2 kmax + (kd == kmax)]
+    v.k255 = v.sinv + 4096;                                         // 256 f64: k / 255.0 (the exact path)
     v.red = v.k255 + 2048;                                          // 16 waves x 8 x u64
     v.code = v.red + 1024;                                          // 65536 u8
     v.rcell = v.code + 65536;                                       // ncell u32
@@ -124,7 +125,10 @@ struct TRead {
 // would wait for it).
 __device__ __forceinline__ TRead t_read(int kmx, int kd, const unsigned char* __restrict__ code8,
                                         const double* __restrict__ inv) {
-    return TRead{code8[(kmx << 8) | kd], inv[max(kd, 1)], inv[kmx]};
+    const double* sinv = inv + 256;
+    // inv[k] = 0.5 / k; sinv[2k] = 1 / k, sinv[2k + 1] = 0.999999 / k (rgb2hsv's
+    // s when min == 0, src/image_processing.c:408-414; within an ulp, for sums)
+    return TRead{code8[(kmx << 8) | kd], inv[max(kd, 1)], sinv[2 * kmx + (kd == kmx ? 1 : 0)]};
 }
 __device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, const TRead& rd,
                                         unsigned long long* __restrict__ cells, double* __restrict__ gs2,
@@ -134,10 +138,10 @@ __device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn
     const double ikd = rd.ikd, imx = rd.imx;
     const bool isr = kr == kmx, isg = kg == kmx;
     const int num = isr ? kg - kb : (isg ? kb - kr : kr - kg);
-    const int t = isr ? (num < 0 ? 3 : 0) : (isg ? 1 : 2);     // base = 120 t
+    const int b2 = isr ? ((num >> 31) & 720) : (isg ? 240 : 480);   // 2 base = 240 t
     // two channels equal <=> num is 0 or +-kd (rgb2hsv's hue is then exact)
     const bool special = (kr == kg) | (kg == kb) | (kr == kb);
-    const int n2 = __mul24(240 * t, kd1) + 120 * num;            // 2N, N = base kd + 60 num
+    const int n2 = __mul24(b2, kd1) + 120 * num;                 // 2N, N = base kd + 60 num
     const int D = __mul24(X.lh, kd1);
     const int c = (int)(((float)n2 + 0.5f) * __builtin_amdgcn_rcpf((float)D));
     const bool onb = __mul24(c, D) == n2;
@@ -155,8 +159,8 @@ __device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn
     const unsigned lo = 1u + ((unsigned)kmx << 16);
     const unsigned hi32 = (unsigned)(kmx + 1) & 256u;            // #(kmax == 255) at bit 40
     if (!(abl & 1)) atomicAdd(&cells[(csel << X.cshift) | X.mycopy], ((unsigned long long)hi32 << 32) | lo);
-    const double h = (double)(n2 >> 1) * ikd;
-    const double s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * imx;
+    const double h = (double)n2 * ikd;                          // (2N) (0.5 / kd) == N (1 / kd)
+    const double s = (double)kd * imx;
     double* a = gs2 + 2 * ((gsel << X.cshift) | X.mycopy);
     if (!(abl & 2)) {
         atomicAdd(a, h);
@@ -202,7 +206,7 @@ __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k2
         g = X.gs + code - X.spvp;
         cell = X.cgs + (code - X.spvp) * X.hp2 + cg;
     }
-    const double s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * inv[kmx];
+    const double s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * inv[256 + 2 * kmx];   // 1 / kmx
     const unsigned lo = 1u + ((unsigned)kmx << 16), hi32 = (unsigned)(kmx + 1) & 256u;
     atomicAdd(&cells[(cell << X.cshift) | X.mycopy], ((unsigned long long)hi32 << 32) | lo);
     double* a = gs2 + 2 * ((g << X.cshift) | X.mycopy);
@@ -299,7 +303,9 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
         uint4* dst = reinterpret_cast<uint4*>(code8);
         for (int i = tid; i < 65536 / 16; i += kT) dst[i] = src[i];
         for (int i = tid; i < 256; i += kT) {
-            inv[i] = tabs->inv[i];
+            inv[i] = 0.5 * tabs->inv[i];                                    // 0.5 / k
+            inv[256 + 2 * i] = tabs->inv[i];                                // 1 / k
+            inv[257 + 2 * i] = i ? 0.999999 / (double)i : 0.0;              // rgb2hsv's 0.999999 (min == 0) / k
             k255[i] = k255g[i];
         }
         unsigned* z = reinterpret_cast<unsigned*>(smem);

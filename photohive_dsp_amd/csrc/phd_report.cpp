@@ -604,8 +604,10 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         // one Kcut and one K3 launch over the whole batch
         PHD_HIP(hipMemcpyAsync(dw + L.E_dev(n), hp + L.E_pin(n), L.e_bytes, hipMemcpyHostToDevice, s2));
         const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(n));
+        // timing experiments only: PHD_ABLATE bit 1024 skips the tail kernels (wrong palette sums)
+        const bool skip_tail = (env_ablate() & 1024) != 0;
         int ps = n_ent ? c->prof.begin(kCutoffs, s2) : -1;
-        PHD_HIP(launch_cutoffs_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
+        if (!skip_tail) PHD_HIP(launch_cutoffs_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
                                      (const int2*)(dw + L.E_dev(n) + L.e_entries), n_ent,
                                      (const unsigned short*)(dw + L.H(n, 0)), (long)L.chunk_bytes,
                                      (GroupRule*)(dw + L.B(n, 0) + L.b_rules), (long)L.b_bytes, s2));
@@ -613,7 +615,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         if (fused) {
             // only the partial groups' kept prefixes are left to sum on the device
             ps = n_ent ? c->prof.begin(kPalSums, s2) : -1;
-            PHD_HIP(launch_partial_sums_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
+            if (!skip_tail) PHD_HIP(launch_partial_sums_batch(d_ptrs, d_imgs, n, height, width, gp, cls->fc, cls->d, c->d_k255,
                                               (const int2*)(dw + L.E_dev(n) + L.e_entries), n_ent,
                                               (const unsigned short*)(dw + L.H(n, 0)), (long)L.chunk_bytes,
                                               (const GroupRule*)(dw + L.B(n, 0) + L.b_rules),
