@@ -41,7 +41,8 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--batch", type=int, default=8, help="images per GPU per step")
+    p.add_argument("--batch", type=int, default=16,
+                   help="images per GPU per step (16: 6.6k images/s against 6.1k at 8, the per-step fixed costs amortised; 24-32 expose the serial host decisions)")
     p.add_argument("--height", type=int, default=3000)
     p.add_argument("--width", type=int, default=4000)
     p.add_argument("--no-cpu-baseline", action="store_true")
