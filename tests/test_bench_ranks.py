@@ -14,7 +14,7 @@ def test_bench_gpus2_spawns_ranks_and_merges_counters():
     env = dict(os.environ, PHD_BENCH_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plan-only",
-                        "--config4-images", "64", "--config5-images", "96"],
+                        "--batch", "8", "--config4-images", "64", "--config5-images", "96"],
                        env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
