@@ -168,6 +168,34 @@ __device__ __forceinline__ void dft(double2 (&v)[R]) {
     dft_ab<split_of(R), R / split_of(R)>(v);
 }
 
+// v[r] *= w^r for r = 1..R-1.  The powers come from four interleaved chains
+// (w^r = w^(r-4) w^4), so the longest dependent run of complex products is
+// about R/4 + 2 instead of R - 1 (latency: the passes run at 2-4 waves per SIMD).
+template <int R>
+__device__ __forceinline__ void twiddle_powers(double2 (&v)[R], const double2 w) {
+    if constexpr (R <= 4) {
+        double2 wr = w;
+        v[1] = cmul(v[1], w);
+#pragma unroll
+        for (int r = 2; r < R; r++) {
+            wr = cmul(wr, w);
+            v[r] = cmul(v[r], wr);
+        }
+    } else {
+        double2 p[4];
+        p[1] = w;
+        p[2] = cmul(w, w);
+        p[3] = cmul(p[2], w);
+        p[0] = cmul(p[2], p[2]);                                  // w^4
+        const double2 w4 = p[0];
+#pragma unroll
+        for (int r = 1; r < R; r++) {
+            if (r > 4) p[r & 3] = cmul(p[r & 3], w4);
+            v[r] = cmul(v[r], p[r & 3]);
+        }
+    }
+}
+
 // ---- one Stockham pass --------------------------------------------------------
 template <int N, int T, int R, int NS>
 struct Pass {
@@ -196,16 +224,7 @@ struct Pass {
             if (active(b)) {
                 if constexpr (NS > 1) {
                     const int jm = b % NS;
-                    if (jm != 0) {
-                        const double2 w = tw[jm];
-                        double2 wr = w;
-                        v[q][1] = cmul(v[q][1], w);
-#pragma unroll
-                        for (int r = 2; r < R; r++) {
-                            wr = cmul(wr, w);
-                            v[q][r] = cmul(v[q][r], wr);
-                        }
-                    }
+                    if (jm != 0) twiddle_powers<R>(v[q], tw[jm]);
                 }
                 dft<R>(v[q]);
             }
