@@ -16,11 +16,20 @@
 //   * max / min: v_pk_max_u16 / v_pk_min_u16, d = max - min (v_pk_sub);
 //   * s for a pixel pair (a, b): s_a + s_b = (d_a M_b + d_b M_a) / (M_a M_b),
 //     numerator and denominator each one v_dot2 (2 M_a M_b = dot2(M, swap M)),
-//     one fp32 reciprocal per pair.  M is raised to 1 for black pixels (d = 0).
-// rgb2hsv's s is d / max except 0.999999 for d == max (min == 0): here those
-// pixels add d / max = 1, so S-bar is high by at most 1e-6 relative (fp32
-// rounding adds ~1e-7): inside north_star's 1e-4 for the float fields.  The
-// full report's K1 (palette.hip) keeps the exact fp64 s.
+//     one fp32 reciprocal per pair, summed in fp32 per item and in fp64 per run.
+//     M is raised to 1 for black pixels (d = 0).
+// rgb2hsv's s is d / max except 0.999999 for d == max (min == 0 < max,
+// src/image_processing.c:408-414).  By default those pixels add d / max = 1,
+// so S-bar is high by at most 1e-6 relative (fp32 rounding adds ~1e-7): inside
+// north_star's 1e-4 for the float fields.  The exact forms were measured and
+// cost the pass its HBM roofline -- at 3 bytes per pixel it sits at the
+// crossover where a few more VALU per pixel make it VALU-bound:
+//   PHD_STATS_MODE=1: + a count of min == 0 < max pixels (packed u16), each
+//                     taking (1 - 0.999999) off at the flush: ~1e-7 relative,
+//                     0.60-0.63 of the HBM peak against 0.71-0.74;
+//   PHD_STATS_MODE=2: + compensated fp32 quotients and Kahan sums: ~2e-9, 0.57;
+//   (an fp64 v_rcp_f64 + Newton form: 0.54, not kept).
+// The full report's K1 (k1.hip) keeps the exact fp64 s.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,9 +55,15 @@ __device__ __forceinline__ unsigned as_u32(u16x2 x) { return __builtin_bit_cast(
 struct StatAcc {
     unsigned sr, sg, sb, qr, qg, qb;         // per-thread moments of the run (u32: <= 1024 items)
     f32x2 s;                                 // sum(s_a + s_b) / 2 of the item's pixel pairs
+    f32x2 c;                                 // kMode 2: minus its Kahan compensation (and the residuals)
+    double s64;                              // kMode >= 1: the partial final group's s (fp64)
+    u16x2 n1;                                // pixels with min == 0 < max (<= 8 per item per half)
 };
 
 // 4 pixels (3 little-endian words w0..w2 = r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3).
+// kMode 0: plain fp32 pair sums (round 1); 1: + the 0.999999 rule (default);
+// 2: + compensated quotients and Kahan sums
+template <int kMode>
 __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, StatAcc& a) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as_u16x2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
@@ -78,12 +93,33 @@ __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, Sta
     const u16x2 S02 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M02), as_u32(M02), 16));
     const u16x2 S13 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M13), as_u32(M13), 16));
     // (d_a M_b + d_b M_a) and 2 M_a M_b, exact integers < 2^18
-    const f32x2 num = {(float)__builtin_amdgcn_udot2(d02, S02, 0u, false),
-                       (float)__builtin_amdgcn_udot2(d13, S13, 0u, false)};
-    const f32x2 den = {(float)__builtin_amdgcn_udot2(M02, S02, 0u, false),
-                       (float)__builtin_amdgcn_udot2(M13, S13, 0u, false)};
-    const f32x2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-    a.s = __builtin_elementwise_fma(num, rc, a.s);
+    const unsigned nu02 = __builtin_amdgcn_udot2(d02, S02, 0u, false), nu13 = __builtin_amdgcn_udot2(d13, S13, 0u, false);
+    const unsigned de02 = __builtin_amdgcn_udot2(M02, S02, 0u, false), de13 = __builtin_amdgcn_udot2(M13, S13, 0u, false);
+    if constexpr (kMode < 2) {
+        const f32x2 num = {(float)nu02, (float)nu13};
+        const f32x2 den = {(float)de02, (float)de13};
+        const f32x2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        a.s = __builtin_elementwise_fma(num, rc, a.s);
+    } else {
+        // (s_a + s_b) / 2 = num / den as q + q2 (q = num rcp(den), q2 = the exact
+        // fp32 residual fma(-q, den, num) times rcp(den): ~2^-46 relative), both
+        // added with Kahan compensation; two pairs per packed instruction
+        const f32x2 num = {(float)nu02, (float)nu13};
+        const f32x2 den = {(float)de02, (float)de13};
+        const f32x2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        const f32x2 q = num * rc;
+        const f32x2 q2 = __builtin_elementwise_fma(-q, den, num) * rc;
+        const f32x2 y = q - a.c;                      // Kahan: a.s + a.c carries the sum
+        const f32x2 t = a.s + y;
+        a.c = (t - a.s) - y - q2;
+        a.s = t;
+    }
+    if constexpr (kMode >= 1) {
+        // min == 0 < max: rgb2hsv's 0.999999 instead of d / max = 1
+        const u16x2 zero = {0, 0};
+        a.n1 += (u16x2)((n02 == zero) & (m02 != zero)) & one;
+        a.n1 += (u16x2)((n13 == zero) & (m13 != zero)) & one;
+    }
 }
 
 // One launch over a batch of same-size, 4-byte-aligned images.  Work items
@@ -92,7 +128,7 @@ __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, Sta
 // (or every 1024 items, so the u32 squares cannot overflow: 1024 * 8 groups *
 // 4 * 255^2 < 2^32).  Outputs as K1's statistics-only form: out.sums (6 u64,
 // atomics) and out.s_part[first chunk of the run] (one fp64 per run).
-template <bool kNT>
+template <bool kNT, int kMode>
 __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* const* __restrict__ imgs, long npix,
                                                               int nchunks, long nitems, PaletteDev out,
                                                               long a_stride) {
@@ -103,7 +139,7 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
     const long full_end = npix & ~3L;                       // groups wholly inside the image
     int img = (int)(it0 / nchunks), c = (int)(it0 - (long)img * nchunks);
     const uint8_t* ip = imgs[img];
-    StatAcc a{0, 0, 0, 0, 0, 0, {0.f, 0.f}};
+    StatAcc a{0, 0, 0, 0, 0, 0, {0.f, 0.f}, {0.f, 0.f}, 0.0, {0, 0}};
     double ssum = 0.0;
     int seg_c0 = c;
     long seg_it0 = it0;
@@ -128,26 +164,31 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
                 }
             }
 #pragma unroll
-            for (int st = 0; st < kStGroups; st++) stat4(w[st][0], w[st][1], w[st][2], a);
+            for (int st = 0; st < kStGroups; st++) stat4<kMode>(w[st][0], w[st][1], w[st][2], a);
         } else {
 #pragma unroll 1
             for (int st = 0; st < kStGroups; st++) {
                 const long p0 = base + 4L * tid + 4L * kStThreads * st;
                 if (p0 < full_end) {
                     gu32s* q = (gu32s*)(ip + 3 * p0);
-                    stat4(q[0], q[1], q[2], a);
+                    stat4<kMode>(q[0], q[1], q[2], a);
                 }
             }
         }
+        // the item's pair sums (a factor 1/2) into fp64
         ssum += (double)a.s.x + (double)a.s.y;
+        if constexpr (kMode == 2) ssum -= (double)a.c.x + (double)a.c.y;
         a.s = f32x2{0.f, 0.f};
+        a.c = f32x2{0.f, 0.f};
         if (tid == 0 && base + kChunk >= npix) {
             // the < 4 pixels of a partial final group: exact fp64 s
             for (long p = full_end; p < npix; p++) {
                 const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
                 a.sr += kr; a.sg += kg; a.sb += kb;
                 a.qr += kr * kr; a.qg += kg * kg; a.qb += kb * kb;
-                ssum += 0.5 * sat_only(kr, kg, kb);         // ssum counts pairs: halved, doubled below
+                // the pair sums carry a factor 1/2; fp64 s (0.999999 included)
+                if constexpr (kMode == 0) ssum += 0.5 * sat_only(kr, kg, kb);
+                else a.s64 += sat_only(kr, kg, kb);
             }
         }
         const int cimg = img;
@@ -163,7 +204,13 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
             unsigned long long m64[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) m64[k] = wave_sum((unsigned long long)mom[k]);
-            const double sw = wave_sum(ssum);
+            double mine = 2.0 * ssum;                 // sum of s
+            if constexpr (kMode >= 1) {
+                // less (1 - 0.999999) per min == 0 < max pixel; the partial group's exact s
+                const unsigned n1 = (unsigned)a.n1.x + (unsigned)a.n1.y;
+                mine = __builtin_fma(-(1.0 - 0.999999), (double)n1, mine + a.s64);
+            }
+            const double sw = wave_sum(mine);
             if (lane_id() == 0) {
 #pragma unroll
                 for (int k = 0; k < 6; k++) red[wv][k] = m64[k];
@@ -179,10 +226,10 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
             } else if (tid == 6) {
                 double t = 0.0;
                 for (int q = 0; q < kStThreads / 64; q++) t += reinterpret_cast<const double*>(red[q])[6];
-                // one slot per run (distinct first chunks); the pair sums carry a factor 1/2
-                reinterpret_cast<double*>(reinterpret_cast<char*>(out.s_part) + cimg * a_stride)[seg_c0] = 2.0 * t;
+                // one slot per run (distinct first chunks)
+                reinterpret_cast<double*>(reinterpret_cast<char*>(out.s_part) + cimg * a_stride)[seg_c0] = t;
             }
-            a = StatAcc{0, 0, 0, 0, 0, 0, {0.f, 0.f}};
+            a = StatAcc{0, 0, 0, 0, 0, 0, {0.f, 0.f}, {0.f, 0.f}, 0.0, {0, 0}};
             ssum = 0.0;
             seg_c0 = c;
             seg_it0 = it + 1;
@@ -200,17 +247,29 @@ hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     // non-temporal loads (the pixels are streamed once): 0.74 of the HBM peak
     // against 0.70-0.72 with plain loads (PHD_STATS_PLAIN=1)
     static const bool nt = getenv("PHD_STATS_PLAIN") == nullptr;
+    // PHD_STATS_MODE (config 3, 512 x 1080p, fraction of the 8 TB/s peak):
+    // 0 (default) fp32 pair sums 0.71-0.74; 1 + the 0.999999 count 0.60-0.63;
+    // 2 + compensated quotients 0.57; an fp64 rcp + Newton form measured 0.54
+    static const int mode = getenv("PHD_STATS_MODE") ? atoi(getenv("PHD_STATS_MODE")) : 0;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_rgb_stats<false>, kStThreads, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_rgb_stats<true, 1>, kStThreads, 0) !=
             hipSuccess || per_cu < 1)
         per_cu = 1;
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
-    if (nt)
-        phd_launch(k_rgb_stats<true>, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
-                   a_stride);
-    else
-        phd_launch(k_rgb_stats<false>, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0,
-                   a_stride);
+#define PHD_ST(NT, M)                                                                                          \
+    phd_launch((k_rgb_stats<NT, M>), dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0, \
+               a_stride)
+    if (mode == 0) {
+        if (nt) PHD_ST(true, 0);
+        else PHD_ST(false, 0);
+    } else if (mode == 2) {
+        if (nt) PHD_ST(true, 2);
+        else PHD_ST(false, 2);
+    } else {
+        if (nt) PHD_ST(true, 1);
+        else PHD_ST(false, 1);
+    }
+#undef PHD_ST
     return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@ within 1e-4 relative (observed ~1e-12: fp64 everywhere, only summation order
 and libm ulps differ).
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -189,7 +190,8 @@ def test_hsv_stats_batch_config3_shape():
 # The statistics-only pass (stats.hip) sums s in fp32 per pixel pair and lets
 # d == max pixels add 1 instead of rgb2hsv's 0.999999: S-bar within 2e-6
 # relative (north_star allows 1e-4 for float fields); the moments are exact.
-STATS_SAT_RTOL = 2e-6
+# PHD_STATS_MODE=1 / 2 (closer forms, slower; stats.hip) are within 3e-7 / 5e-9.
+STATS_SAT_RTOL = {0: 2e-6, 1: 3e-7, 2: 5e-9}[int(os.environ.get("PHD_STATS_MODE", "0"))]
 
 
 @pytest.mark.parametrize("kind,h,w", [("uniform", 401, 577), ("black", 400, 400), ("saturated", 360, 1200),
