@@ -6,7 +6,7 @@ set -e
 TAG="${1:-r02}"
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python tools/pmc_collect.py --tag "${TAG:-r02}" -- --steps 3 --warmup 1 --no-config3 > gpurun_out/pmc_collect.log 2>&1
+timeout -k 10 300 python tools/pmc_collect.py --tag "${TAG:-r02}" -- --steps 3 --warmup 1 --no-config3 --batch 8 > gpurun_out/pmc_collect.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof2 -o prof -- python bench.py --no-config3 --no-cpu-baseline > gpurun_out/bench_prof2.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline > gpurun_out/bench_prof.log 2>&1
 timeout -k 10 300 python bench.py > gpurun_out/bench_full.log 2>&1
