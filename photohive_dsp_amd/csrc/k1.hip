@@ -31,10 +31,11 @@
 // chunk's classification by its own thread in fp64 (t_exact, palette.hip's
 // fused_exact decisions).
 //
-// One block of 1024 threads per CU (the table takes 64 KiB of LDS); each
-// block walks a contiguous run of (image, 16384-pixel chunk) items, 16 pixels
-// per thread per chunk, the next chunk's loads issued before the current
-// chunk's fold.
+// Persistent blocks: one of 1024 threads per CU (the full code table takes
+// 64 KiB of LDS), or two of 512 threads (the triangular table, below); each
+// block walks a contiguous run of (image, 16384-pixel chunk) items, 16 or 32
+// pixels per thread per chunk, the next chunk's loads issued before the
+// current chunk's fold.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,18 +47,25 @@ namespace phd {
 
 namespace {
 
-#ifndef PHD_K1_T
-#define PHD_K1_T 1024
-#endif
-constexpr int kT = PHD_K1_T;                              // threads per block
-constexpr int kG = kChunk / (4 * kT);                     // 4-pixel groups per thread per chunk
-static_assert(kG == 4 || kG == 8, "K1 tile");
+// Two forms (k1t_cshift / k1t_cshift2): one 1024-thread block per CU with the
+// full 256 x 256 code table, or -- when the grid's records fit 79 KiB -- two
+// 512-thread blocks per CU with the kd <= kmax triangle of the table (32896
+// bytes): the same 16 waves per CU, but the two blocks' barriers and chunk
+// folds no longer stall each other (K1 716 against 758 us per 16 images).
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) unsigned gu32t;
 
 __device__ __forceinline__ u16x2 as2(unsigned x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ unsigned as1(u16x2 x) { return __builtin_bit_cast(unsigned, x); }
+
+template <bool TRI>
+constexpr int code_bytes() { return TRI ? 256 * 257 / 2 : 65536; }
+template <bool TRI>
+__device__ __forceinline__ int code_idx(int kmx, int kd) {
+    if constexpr (TRI) return (int)(__umul24(kmx, kmx + 1) >> 1) + kd;
+    else return (kmx << 8) | kd;
+}
 
 // LDS carve (bytes).  Every base a pixel touches (cells, h/s sums, the
 // reciprocals, the code tables) lies below 64 KiB, so it is a DS
@@ -66,7 +74,7 @@ __device__ __forceinline__ unsigned as1(u16x2 x) { return __builtin_bit_cast(uns
 struct TVar {
     int cells, gs2, ce, inv, sinv, k255, red, code, rcell, cg, seg, r255, rmx, end;
 };
-__host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
+__host__ __device__ inline TVar t_var(int tl, int ncell, int cshift, int code_bytes) {
     const int C = 1 << cshift;
     TVar v;
     v.cells = 0;                                                    // (ncell+1) * C u64
@@ -76,8 +84,8 @@ __host__ __device__ inline TVar t_var(int tl, int ncell, int cshift) {
     v.sinv = v.inv + 2048;                                          // 512 f64: s = kd * sinv[2 kmax + (kd == kmax)]
     v.k255 = v.sinv + 4096;                                         // 256 f64: k / 255.0 (the exact path)
     v.red = v.k255 + 2048;                                          // 16 waves x 8 x u64
-    v.code = v.red + 1024;                                          // 65536 u8
-    v.rcell = v.code + 65536;                                       // ncell u32
+    v.code = v.red + 1024;                                          // code_bytes u8
+    v.rcell = v.code + code_bytes;                                  // ncell u32
     v.cg = v.rcell + 4 * ncell;                                     // tl u32
     v.seg = v.cg + 4 * tl;                                          // tl u32
     v.r255 = v.seg + 4 * tl;                                        // tl u32
@@ -123,12 +131,13 @@ struct TRead {
 // The pixel's three table reads (issued for a whole 4-pixel group before its
 // atomics: LDS operations complete in order, so a read placed after an atomic
 // would wait for it).
+template <bool TRI>
 __device__ __forceinline__ TRead t_read(int kmx, int kd, const unsigned char* __restrict__ code8,
                                         const double* __restrict__ inv) {
     const double* sinv = inv + 256;
     // inv[k] = 0.5 / k; sinv[2k] = 1 / k, sinv[2k + 1] = 0.999999 / k (rgb2hsv's
     // s when min == 0, src/image_processing.c:408-414; within an ulp, for sums)
-    return TRead{code8[(kmx << 8) | kd], inv[max(kd, 1)], sinv[2 * kmx + (kd == kmx ? 1 : 0)]};
+    return TRead{code8[code_idx<TRI>(kmx, kd)], inv[max(kd, 1)], sinv[2 * kmx + (kd == kmx ? 1 : 0)]};
 }
 __device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, const TRead& rd,
                                         unsigned long long* __restrict__ cells, double* __restrict__ gs2,
@@ -177,6 +186,7 @@ __device__ __forceinline__ bool t_pixel(int kr, int kg, int kb, int kmx, int kmn
 // the hue bin is arm_octree's (int)(h / Lh) (src/color_quantization.c:143)
 // and the cell the side of B_c calculate_avg_hsv's wrap test puts h on, as
 // palette.hip's fused_exact.
+template <bool TRI>
 __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k255g, const GridParams& gp,
                                         const unsigned char* code8, const double* inv,
                                         unsigned long long* cells, double* gs2, const TConst& X) {
@@ -196,7 +206,7 @@ __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k2
     else if (ch & 1) below = (int)!((h + (360.0 - B)) > 360);             // off = 360 - B
     else below = 0;
     const int cg = c - below;
-    const int code = code8[(kmx << 8) | kd];
+    const int code = code8[code_idx<TRI>(kmx, kd)];
     int g, cell;
     if (code < X.spvp) {
         const int hi = (int)(h / gp.Lh);
@@ -226,6 +236,7 @@ struct Mom {
 
 // 4 pixels: moments (packed), then each pixel classified; bit i of the
 // result = pixel i deferred.
+template <bool TRI>
 __device__ __forceinline__ unsigned t_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
                                             const unsigned char* __restrict__ code8, const double* __restrict__ inv,
                                             unsigned long long* __restrict__ cells, double* __restrict__ gs2,
@@ -262,7 +273,7 @@ __device__ __forceinline__ unsigned t_group(unsigned w0, unsigned w1, unsigned w
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);               // pixel i: pair q, half i >> 1
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF;
-        rd[i] = t_read(kmx, kmx - kmn, code8, inv);
+        rd[i] = t_read<TRI>(kmx, kmx - kmn, code8, inv);
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -274,7 +285,8 @@ __device__ __forceinline__ unsigned t_group(unsigned w0, unsigned w1, unsigned w
     return def;
 }
 
-__global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict__ imgs, long npix, int nchunks,
+template <int KT, bool TRI>
+__global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict__ imgs, long npix, int nchunks,
                                                long nitems, GridParams gp, const ClassTables* __restrict__ tabs,
                                                const double* __restrict__ k255g, PaletteDev out, long a_stride,
                                                long h_stride, int cshift, int ablate_arg) {
@@ -286,7 +298,9 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
     if (it0 >= it1) return;                                     // block-uniform
     const int C = 1 << cshift, cm = C - 1;
     const TConst X = make_tconst(gp, cshift, tid & cm);
-    const TVar V = t_var(X.tl, X.ncell, cshift);
+    constexpr int kT = KT, kG = kChunk / (4 * KT);              // threads; 4-pixel groups per thread per chunk
+    static_assert(kG == 4 || kG == 8, "K1 tile");
+    const TVar V = t_var(X.tl, X.ncell, cshift, code_bytes<TRI>());
     unsigned char* code8 = smem + V.code;
     double* inv = reinterpret_cast<double*>(smem + V.inv);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + V.red);
@@ -299,9 +313,10 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
     unsigned long long* rmx = reinterpret_cast<unsigned long long*>(smem + V.rmx);
     double* k255 = reinterpret_cast<double*>(smem + V.k255);
     {
-        const uint4* src = reinterpret_cast<const uint4*>(tabs->code8);
+        static_assert(code_bytes<TRI>() % 16 == 0, "uint4 copy");
+        const uint4* src = reinterpret_cast<const uint4*>(TRI ? tabs->code_tri : tabs->code8);
         uint4* dst = reinterpret_cast<uint4*>(code8);
-        for (int i = tid; i < 65536 / 16; i += kT) dst[i] = src[i];
+        for (int i = tid; i < code_bytes<TRI>() / 16; i += kT) dst[i] = src[i];
         for (int i = tid; i < 256; i += kT) {
             inv[i] = 0.5 * tabs->inv[i];                                    // 0.5 / k
             inv[256 + 2 * i] = tabs->inv[i];                                // 1 / k
@@ -366,7 +381,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
         unsigned emask = 0;                                       // deferred pixels (bit 4 st + i)
 #pragma unroll
         for (int st = 0; st < kG; st++)
-            emask |= t_group(cw[st][0], cw[st][1], cw[st][2], m, code8, inv, cells, gs2, X, abl) << (4 * st);
+            emask |= t_group<TRI>(cw[st][0], cw[st][1], cw[st][2], m, code8, inv, cells, gs2, X, abl) << (4 * st);
         if (abl & 4) emask = 0;
         const bool last_chunk = base + kChunk >= npix;            // block-uniform
         if (last_chunk && tid == 0) {
@@ -376,8 +391,8 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
                 m.sr += kr; m.sg += kg; m.sb += kb;
                 m.qr += kr * kr; m.qg += kg * kg; m.qb += kb * kb;
                 const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
-                if (t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, t_read(kmx, kmx - kmn, code8, inv), cells, gs2, X, 0))
-                    t_exact(kr, kg, kb, k255, gp, code8, inv, cells, gs2, X);
+                if (t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, t_read<TRI>(kmx, kmx - kmn, code8, inv), cells, gs2, X, 0))
+                    t_exact<TRI>(kr, kg, kb, k255, gp, code8, inv, cells, gs2, X);
             }
         }
         // deferred pixels (a hue exactly on a half-bin boundary, ~1.7 % of uniform
@@ -396,7 +411,7 @@ __global__ __launch_bounds__(kT, 4) void k_k1t(const uint8_t* const* __restrict_
                     a1 = cw[st][1];
                     a2 = cw[st][2];
                 }
-            t_exact(group_byte(a0, a1, a2, 3 * pi), group_byte(a0, a1, a2, 3 * pi + 1),
+            t_exact<TRI>(group_byte(a0, a1, a2, 3 * pi), group_byte(a0, a1, a2, 3 * pi + 1),
                     group_byte(a0, a1, a2, 3 * pi + 2), k255, gp, code8, inv, cells, gs2, X);
         }
         const long pad = base + kChunk - full_end;                // zero pixels of masked groups
@@ -510,26 +525,44 @@ int k1t_cshift(const GridParams& gp, const ClassTables& t) {
     const int ncell = HueCells::count(gp);
     static const int budget = getenv("PHD_K1_LDS_KB") ? atoi(getenv("PHD_K1_LDS_KB")) : 158;
     for (int cs = 4; cs >= 0; cs--)
-        if (t_var(gp.tl, ncell, cs).end <= budget * 1024) return cs;
+        if (t_var(gp.tl, ncell, cs, code_bytes<false>()).end <= budget * 1024) return cs;
+    return -1;
+}
+
+int k1t_cshift2(const GridParams& gp, const ClassTables& t) {
+    if (!t.codes_ok || getenv("PHD_K1_ONE_BLOCK")) return -1;
+    const int ncell = HueCells::count(gp);
+    for (int cs = 4; cs >= 2; cs--)                       // >= 4 lane copies (fewer: bank conflicts)
+        if (t_var(gp.tl, ncell, cs, code_bytes<true>()).end <= 79 * 1024) return cs;
     return -1;
 }
 
 hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int width, const GridParams& gp,
                             const ClassTables* tabs, const PaletteDev& out0, long a_stride, long h_stride,
-                            int nchunks, const double* k255, int cshift, hipStream_t st) {
+                            int nchunks, const double* k255, int cshift, int cshift2, hipStream_t st) {
     const long npix = (long)height * width;
     const long nitems = (long)n * nchunks;
-    const size_t lds = (size_t)t_var(gp.tl, HueCells::count(gp), cshift).end;
+    const int ncell = HueCells::count(gp);
     static bool attr = false;
     if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_k1t, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_k1t<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_k1t<512, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         attr = true;
     }
-    const int grid = (int)std::min<long>(nitems, (long)num_cus());
-    phd_launch(k_k1t, dim3(grid), dim3(kT), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255, out0,
-                       a_stride, h_stride, cshift, g_ablate | env_ablate());
+    if (cshift2 >= 0) {                                   // two 512-thread blocks per CU
+        const size_t lds = (size_t)t_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
+        const int grid = (int)std::min<long>(nitems, 2L * num_cus());
+        phd_launch((k_k1t<512, true>), dim3(grid), dim3(512), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255,
+                   out0, a_stride, h_stride, cshift2, g_ablate | env_ablate());
+    } else {                                              // one 1024-thread block per CU
+        const size_t lds = (size_t)t_var(gp.tl, ncell, cshift, code_bytes<false>()).end;
+        const int grid = (int)std::min<long>(nitems, (long)num_cus());
+        phd_launch((k_k1t<1024, false>), dim3(grid), dim3(1024), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs,
+                   k255, out0, a_stride, h_stride, cshift, g_ablate | env_ablate());
+    }
     return hipGetLastError();
 }
 
 }  // namespace phd
-

@@ -1421,7 +1421,7 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     // the fused palette pass over word-aligned images: the table K1 (k1.hip)
     if (sums && aligned && fc.k1t_cshift >= 0 && !getenv("PHD_K1_OLD"))
         return launch_k1t_batch(d_imgs, n, height, width, gp, tabs, out0, a_stride, h_stride, nchunks, k255,
-                                fc.k1t_cshift, st);
+                                fc.k1t_cshift, fc.k1t_cshift2, st);
     // the statistics-only pass over word-aligned images: the lean kernel (stats.hip)
     if (!hist && aligned && !getenv("PHD_STATS_K1"))
         return launch_rgb_stats_batch(d_imgs, n, height, width, out0, a_stride, nchunks, st);

@@ -60,6 +60,7 @@ struct FastCls {
     int lh;                    // Lh = 360 / h_partitions (integer division, :41)
     int use_thr;               // Si from ClsEnt::thr (s_partitions <= 6), else si8 in global memory
     int k1t_cshift = -1;       // the table K1 (k1.hip) fits this grid with 1 << k1t_cshift copies
+    int k1t_cshift2 = -1;      // ... as two 512-thread blocks per CU (triangular code table), else -1
 };
 // Si is non-decreasing in kd = kmax - kmin for a fixed kmax (s = d / max is), so
 // it is -1 plus the number of thresholds kd reaches.
@@ -78,6 +79,7 @@ struct ClassTables {           // device copy; ent is staged into LDS by the ker
     // group's (Si, Vi) as Si * vp + Vi, else sp * vp + (gray / black group -
     // gray_start)
     unsigned char code8[256 * 256];
+    unsigned char code_tri[256 * 257 / 2];   // the same codes, kd <= kmax only: [kmax (kmax + 1) / 2 + kd]
     double inv[256];              // 1.0 / k (inv[0] = 0)
     int codes_ok;                 // every (kmax, kd) got a code (sp * vp + ng + 1 <= 256)
 };
@@ -157,9 +159,10 @@ hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
 // lane-private copies, or -1 when this grid does not fit it (palette.hip's
 // fused K1 then runs).
 int k1t_cshift(const GridParams& gp, const ClassTables& host_tabs);
+int k1t_cshift2(const GridParams& gp, const ClassTables& host_tabs);
 hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int width, const GridParams& gp,
                             const ClassTables* tabs, const PaletteDev& out0, long a_stride, long h_stride,
-                            int nchunks, const double* k255, int cshift, hipStream_t st);
+                            int nchunks, const double* k255, int cshift, int cshift2, hipStream_t st);
 // The fused K1's LDS fits this grid (else the palette uses K1 + K3).
 bool fused_palette_ok(const GridParams& gp);
 // Fused palette: the slot sums of the partial (tie-overflow) groups, added

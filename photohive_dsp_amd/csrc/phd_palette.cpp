@@ -135,11 +135,13 @@ void make_class_tables(const GridParams& g, FastCls* fc, ClassTables* t) {
             else code = si * g.vp + vcol;
             if (code < 0 || code > 255) t->codes_ok = 0;
             t->code8[k * 256 + kd] = (unsigned char)code;
+            t->code_tri[k * (k + 1) / 2 + kd] = (unsigned char)code;
         }
     }
     t->inv[0] = 0.0;
     for (int k = 1; k < 256; k++) t->inv[k] = 1.0 / (double)k;
     fc->k1t_cshift = k1t_cshift(g, *t);
+    fc->k1t_cshift2 = fc->k1t_cshift >= 0 ? k1t_cshift2(g, *t) : -1;
 }
 
 namespace {
