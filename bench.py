@@ -39,7 +39,7 @@ METRIC = "images/sec (4000×3000 RGB8 full report) at 1/2/4/8 GPUs; HBM GB/s vs 
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=16,
                    help="images per GPU per step (16: 6.6k images/s against 6.1k at 8, the per-step fixed costs amortised; 24-32 expose the serial host decisions)")
