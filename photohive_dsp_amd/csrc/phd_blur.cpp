@@ -9,6 +9,7 @@
 //    10 vectors out -- tiny, sequential, host C++;
 //  * get_blur_profile_visual (src/blur_profile.c:140-180), the third
 //    exported symbol of the reference library.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <thread>
@@ -158,22 +159,39 @@ extern "C" Image_PGM* get_blur_profile_visual(Blur_Profile* bp, int height, int 
         return nullptr;
     }
     Image_PGM* img = (Image_PGM*)malloc(sizeof(Image_PGM));
+    if (!img) return nullptr;
     img->height = height;
     img->width = width;
-    img->data = (Pixel*)calloc((size_t)height * width, sizeof(Pixel));
-    for (int y = 0; y < height; y++)
-        for (int x = 0; x < width; x++) {
-            const double dx = x;
-            const double dy = (y < height / 2) ? -y : (double)(height - y);
-            const double r = std::sqrt(dx * dx + dy * dy);
-            const double phi = std::atan2(dy, dx);
-            int rb = (int)(r / bp->radius_bin_size);
-            if (rb >= bp->num_radius_bins) rb = bp->num_radius_bins - 1;
-            int pb = (int)((phi + phd::kRefPi * 0.5f) / phd::kRefPi * (double)(bp->num_angle_bins - 1));
-            if (pb >= bp->num_angle_bins) pb = bp->num_angle_bins - 1;
-            if (pb < 0) pb = 0;
-            img->data[(size_t)y * width + x] = bp->bins[pb][rb];
-        }
+    img->data = (Pixel*)malloc((size_t)height * width * sizeof(Pixel));
+    if (!img->data) {
+        free(img);
+        phd::set_error("get_blur_profile_visual: out of memory");
+        return nullptr;
+    }
+    // independent per element: blocks of rows on the host pool (every element
+    // is the same sequence of double operations as the reference's loop)
+    constexpr int kRows = 64;
+    auto rows = [&](int blk) {
+        const int y1 = std::min(height, (blk + 1) * kRows);
+        for (int y = blk * kRows; y < y1; y++)
+            for (int x = 0; x < width; x++) {
+                const double dx = x;
+                const double dy = (y < height / 2) ? -y : (double)(height - y);
+                const double r = std::sqrt(dx * dx + dy * dy);
+                const double phi = std::atan2(dy, dx);
+                int rb = (int)(r / bp->radius_bin_size);
+                if (rb >= bp->num_radius_bins) rb = bp->num_radius_bins - 1;
+                int pb = (int)((phi + phd::kRefPi * 0.5f) / phd::kRefPi * (double)(bp->num_angle_bins - 1));
+                if (pb >= bp->num_angle_bins) pb = bp->num_angle_bins - 1;
+                if (pb < 0) pb = 0;
+                img->data[(size_t)y * width + x] = bp->bins[pb][rb];
+            }
+    };
+    const int nblk = (height + kRows - 1) / kRows;
+    phd::HostPool* pool = phd::host_pool();
+    if (pool->size() > 0 && (long)height * width >= (1L << 16)) pool->parallel_for(nblk, rows);
+    else
+        for (int b = 0; b < nblk; b++) rows(b);
     return img;
 }
 
