@@ -316,6 +316,40 @@ def single_image(cx, h=3000, w=4000, iters=20):
     return {"workload": f"1 x {h}x{w} RGB8 per call, full report, median of {iters}", **res}
 
 
+def legacy_entry(cx, h=3000, w=4000, iters=5):
+    """The reference's own binding path (lib.py:25-34, core.py:456-476): three
+    planes of doubles k / 255.0 in host memory -> get_full_report_data ->
+    Full_Report_Data (the planes' 288 MB H2D, the k/255 test and the RGB8
+    pipeline on the device).  Median of `iters` calls; the Python-side
+    pil_image_to_image_rgb (utils.py:30-46) is not included."""
+    import numpy as np
+    lib, torch = cx.lib, cx.torch
+    from photohive_dsp_amd.structures import Image_RGB
+    nb = h * w * 3
+    t = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    cx.fill(t, 4242)
+    rgb = t.cpu().numpy().reshape(h, w, 3)
+    del t
+    planes = [np.ascontiguousarray(rgb[:, :, c]).ravel() / 255.0 for c in range(3)]
+    P = ctypes.POINTER(ctypes.c_double)
+    im = Image_RGB(height=h, width=w, r=planes[0].ctypes.data_as(P), g=planes[1].ctypes.data_as(P),
+                   b=planes[2].ctypes.data_as(P))
+    times = []
+    for k in range(iters + 1):
+        t0 = time.perf_counter()
+        ptr = lib.get_full_report_data(ctypes.byref(im), None, 18, 2, 3, 0.1, 0.1, 0.95, 1000, 1, 40, 72,
+                                       0.1, 0.9, 1.20, 0.3, 2)
+        dt = time.perf_counter() - t0
+        if not ptr:
+            raise RuntimeError(cx.last_error())
+        lib.free_full_report(ctypes.byref(ptr))
+        if k:
+            times.append(dt)
+    times.sort()
+    return {"workload": f"1 x {h}x{w} planar doubles k/255 (host) -> get_full_report_data, median of {iters}",
+            "ms": round(1000 * times[len(times) // 2], 3)}
+
+
 def host_buffers(cx, h=3000, w=4000, n=64, iters=3):
     """SURVEY.md 8(d)'s end-to-end timed region: u8 HOST buffers in ->
     Full_Report_Data out, through phd_report_batch_u8 (PCIe H2D included).
@@ -582,6 +616,7 @@ def main(argv=None):
         if world == 1:
             extra["config2_single"] = single_image(cx, args.height, args.width)
             extra["host_buffer"] = host_buffers(cx, args.height, args.width)
+            extra["legacy_entry"] = legacy_entry(cx, args.height, args.width)
             extra["config3"] = config3(cx)
     if rank == 0:
         m = hl["merged"]
