@@ -71,6 +71,7 @@ Context* get_context() {
     if (hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_k1, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_dl_sd, hipEventDisableTiming) != hipSuccess ||
         hipStreamCreateWithFlags(&c->fft, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_ws, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fft, hipEventDisableTiming) != hipSuccess ||

@@ -180,6 +180,7 @@ struct Context {
     // stream, concurrent with the FFTs: joined by events
     hipStream_t tail = nullptr;
     hipEvent_t ev_k1 = nullptr, ev_tail = nullptr;
+    hipEvent_t ev_dl_sd = nullptr;                  // the download stream's last copy of a call
     // the FFTs run on their own stream too: the compile-time row pass does not
     // need K1, so it overlaps it (only the column pass waits for the sums)
     hipStream_t fft = nullptr;

@@ -433,21 +433,20 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     PHD_HIP(hipEventRecord(c->ev_k1, st));
     PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, st));
     PHD_HIP(hipEventRecord(c->ev[5], st));
-    // the FFTs on their stream: compile-time row passes start with K1, the
-    // column passes (DC removal) wait for it; runtime-plan rows need it too
-    // (PHD_FFT_OVERLAP=1 lets the row passes start with K1; measured no faster,
-    // since K1's persistent blocks leave no room for them, and it blurs the
-    // per-kernel event timings, so by default the FFTs follow K1)
-    const hipStream_t sf = c->fft;
     // PHD_FFT_OVERLAP=1 (compile-time plans): the row pass sums the channels
     // itself (the column pass's DC bias), so the FFT chain needs nothing from
-    // K1 and runs beside it.  Measured slower (5.75k vs 6.05k images/s: row
-    // passes sharing CUs with K1 take 92 us instead of 49), so by default the
-    // FFTs follow K1 and take its channel sums.
+    // K1 and runs beside it on its own stream.  Measured slower (5.75k vs 6.05k
+    // images/s: row passes sharing CUs with K1 take 92 us instead of 49), so by
+    // default the FFTs follow K1 (and its records' download) on K1's stream and
+    // take its channel sums: a cross-stream event wait left the GPU idle
+    // ~20 us between K1 and the first row pass.
     static const bool overlap = getenv("PHD_FFT_OVERLAP") != nullptr;
     const bool own_dc = fs.ct && overlap;
-    PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
-    if (!own_dc) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+    const hipStream_t sf = (pipe || own_dc) ? c->fft : st;
+    if (sf != st) {
+        PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
+        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+    }
     const size_t inter_elems = inter_one / sizeof(double2);
     const hipStream_t sc = c->fft2;
     if (pipe) {
@@ -512,7 +511,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                                     c->d_inter + (size_t)(i - g0) * inter_elems, sf, rsum));
             c->prof.end(ps, sf);
         }
-        if (g0 == 0 && fs.ct && !own_dc) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+        if (g0 == 0 && fs.ct && !own_dc && sf != st) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = own_dc ? (const unsigned long long*)(dw + L.C(n, i) + L.c_rsum)
                                                     : (const unsigned long long*)(dw + L.A(i) + L.a_sums);
@@ -651,23 +650,40 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     }
     PHD_HIP(hipEventRecord(c->ev_tail, s2));
     PHD_HIP(hipStreamWaitEvent(st, c->ev_tail, 0));
-    PHD_HIP(hipStreamWaitEvent(st, c->ev_fft, 0));
+    if (sf != st || pipe) PHD_HIP(hipStreamWaitEvent(st, c->ev_fft, 0));
     PHD_HIP(hipEventRecord(c->ev[3], st));
     // image i's C record (bins, max partials, palette sums, sharpness) goes to
     // the host once its column pass and the palette tail are done; the host
     // assembles it while the later images' FFTs run
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
+    // (the last group's download follows the last column pass on its own
+    // stream when that is K1's: no cross-stream wait at the end of the call)
     const hipStream_t sd = c->dl;
+    const bool last_on_st = sf == st && !pipe;
     PHD_HIP(hipStreamWaitEvent(sd, c->ev_tail, 0));
+    bool sd_used = false;
     for (int i0 = 0; i0 < n; i0 = dl_last(i0) + 1) {
         const int i1 = dl_last(i0);
-        PHD_HIP(hipStreamWaitEvent(sd, c->ev_img_fft[i1], 0));
+        const bool on_st = last_on_st && i1 == n - 1;
+        const hipStream_t s_dl = on_st ? st : sd;
+        if (!on_st) {
+            PHD_HIP(hipStreamWaitEvent(sd, c->ev_img_fft[i1], 0));
+            sd_used = true;
+        }
         PHD_HIP(hipMemcpyAsync(hc + (size_t)i0 * L.c_bytes, dw + L.C(n, i0), (size_t)(i1 - i0 + 1) * L.c_bytes,
-                               hipMemcpyDeviceToHost, sd));
-        PHD_HIP(hipEventRecord(c->ev_img_dl[i1], sd));
+                               hipMemcpyDeviceToHost, s_dl));
+        PHD_HIP(hipEventRecord(c->ev_img_dl[i1], s_dl));
     }
-    PHD_HIP(hipEventRecord(c->ev[4], sd));
-    PHD_HIP(hipStreamWaitEvent(st, c->ev[4], 0));
+    if (last_on_st) {
+        if (sd_used) {
+            PHD_HIP(hipEventRecord(c->ev_dl_sd, sd));
+            PHD_HIP(hipStreamWaitEvent(st, c->ev_dl_sd, 0));
+        }
+        PHD_HIP(hipEventRecord(c->ev[4], st));
+    } else {
+        PHD_HIP(hipEventRecord(c->ev[4], sd));
+        PHD_HIP(hipStreamWaitEvent(st, c->ev[4], 0));
+    }
     const auto t_dec = std::chrono::steady_clock::now();
     auto t_sync = t_dec;
 
