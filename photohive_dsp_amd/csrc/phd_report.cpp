@@ -41,11 +41,12 @@ struct Layout {
     size_t A(int i) const { return (size_t)i * a_bytes; }
     size_t C(int n, int i) const { return (size_t)n * a_bytes + (size_t)i * c_bytes; }
     size_t B(int n, int i) const { return (size_t)n * (a_bytes + c_bytes) + (size_t)i * b_bytes; }
-    size_t H(int n, int i) const { return (size_t)n * (a_bytes + c_bytes + b_bytes) + (size_t)i * chunk_bytes; }
-    size_t P_dev(int n) const { return (size_t)n * (a_bytes + c_bytes + b_bytes + chunk_bytes); }
-    size_t P_pin(int n) const { return (size_t)n * (a_bytes + c_bytes + b_bytes); }
-    size_t E_dev(int n) const { return P_dev(n) + ptr_bytes; }
-    size_t E_pin(int n) const { return P_pin(n) + ptr_bytes; }
+    // E follows the B records on both sides, so one H2D copy carries both
+    size_t E_dev(int n) const { return (size_t)n * (a_bytes + c_bytes + b_bytes); }
+    size_t E_pin(int n) const { return E_dev(n); }
+    size_t H(int n, int i) const { return E_dev(n) + e_bytes + (size_t)i * chunk_bytes; }
+    size_t P_dev(int n) const { return H(n, n); }
+    size_t P_pin(int n) const { return E_pin(n) + e_bytes; }
 };
 
 // ncell > 0: the fused palette's per-group sums and hue-cell counts ride in
@@ -597,11 +598,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const hipStream_t s2 = c->tail;
     PHD_HIP(hipStreamWaitEvent(s2, c->ev_k1, 0));
     uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
-    PHD_HIP(hipMemcpyAsync(dw + L.B(n, 0), hb, (size_t)n * L.b_bytes, hipMemcpyHostToDevice, s2));
     const bool batched = ds <= 1 && (fused || palette_sums_b_lds(gp.tl, max_slots) <= 160 * 1024);
+    // the B records (and, batched, the Kcut list right after them): one copy
+    PHD_HIP(hipMemcpyAsync(dw + L.B(n, 0), hb, (size_t)n * L.b_bytes + (batched ? L.e_bytes : 0),
+                           hipMemcpyHostToDevice, s2));
     if (batched) {
         // one Kcut and one K3 launch over the whole batch
-        PHD_HIP(hipMemcpyAsync(dw + L.E_dev(n), hp + L.E_pin(n), L.e_bytes, hipMemcpyHostToDevice, s2));
         const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(n));
         // timing experiments only: PHD_ABLATE bit 1024 skips the tail kernels (wrong palette sums)
         const bool skip_tail = (env_ablate() & 1024) != 0;
@@ -649,23 +651,33 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         }
     }
     PHD_HIP(hipEventRecord(c->ev_tail, s2));
-    PHD_HIP(hipStreamWaitEvent(st, c->ev_tail, 0));
-    if (sf != st || pipe) PHD_HIP(hipStreamWaitEvent(st, c->ev_fft, 0));
-    PHD_HIP(hipEventRecord(c->ev[3], st));
+    // the stream that finishes last downloads the last results after an event
+    // of the other that is already complete (waiting on a pending event from
+    // another stream costs ~30 us of idle GPU): a single image's palette tail
+    // (decisions, Kcut, partial sums) ends after its FFTs, a batch's FFTs end
+    // after the tail
+    const bool last_on_st = sf == st && !pipe;
+    const bool tail_last = last_on_st && n == 1;
+    if (!tail_last) {
+        PHD_HIP(hipStreamWaitEvent(st, c->ev_tail, 0));
+        if (sf != st || pipe) PHD_HIP(hipStreamWaitEvent(st, c->ev_fft, 0));
+        PHD_HIP(hipEventRecord(c->ev[3], st));
+    } else {
+        PHD_HIP(hipStreamWaitEvent(s2, c->ev_fft, 0));
+        PHD_HIP(hipEventRecord(c->ev[3], s2));
+    }
     // image i's C record (bins, max partials, palette sums, sharpness) goes to
     // the host once its column pass and the palette tail are done; the host
     // assembles it while the later images' FFTs run
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
-    // (the last group's download follows the last column pass on its own
-    // stream when that is K1's: no cross-stream wait at the end of the call)
     const hipStream_t sd = c->dl;
-    const bool last_on_st = sf == st && !pipe;
+    const hipStream_t s_end = tail_last ? s2 : st;           // last_on_st: the last group's stream
     PHD_HIP(hipStreamWaitEvent(sd, c->ev_tail, 0));
     bool sd_used = false;
     for (int i0 = 0; i0 < n; i0 = dl_last(i0) + 1) {
         const int i1 = dl_last(i0);
         const bool on_st = last_on_st && i1 == n - 1;
-        const hipStream_t s_dl = on_st ? st : sd;
+        const hipStream_t s_dl = on_st ? s_end : sd;
         if (!on_st) {
             PHD_HIP(hipStreamWaitEvent(sd, c->ev_img_fft[i1], 0));
             sd_used = true;
@@ -677,9 +689,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (last_on_st) {
         if (sd_used) {
             PHD_HIP(hipEventRecord(c->ev_dl_sd, sd));
-            PHD_HIP(hipStreamWaitEvent(st, c->ev_dl_sd, 0));
+            PHD_HIP(hipStreamWaitEvent(s_end, c->ev_dl_sd, 0));
         }
-        PHD_HIP(hipEventRecord(c->ev[4], st));
+        PHD_HIP(hipEventRecord(c->ev[4], s_end));   // the host waits on it before returning
     } else {
         PHD_HIP(hipEventRecord(c->ev[4], sd));
         PHD_HIP(hipStreamWaitEvent(st, c->ev[4], 0));
