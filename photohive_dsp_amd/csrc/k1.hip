@@ -551,7 +551,14 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                                   160 * 1024);
         attr = true;
     }
-    if (cshift2 >= 0) {                                   // two 512-thread blocks per CU
+    // the two-block form runs a chunk in ~1.9x the time of the one-block form
+    // (half a CU each): it wins when it has at least ~2 chunks per block
+    // (measured at 16 x 732 chunks), not for a single image's 732 chunks
+    // where its last chunks form the tail (3 x 1 against 2 x 1.9)
+    const long cus = num_cus();
+    const bool two = cshift2 >= 0 &&
+                     (cshift < 0 || 19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus));
+    if (two) {                                            // two 512-thread blocks per CU
         const size_t lds = (size_t)t_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
         const int grid = (int)std::min<long>(nitems, 2L * num_cus());
         phd_launch((k_k1t<512, true>), dim3(grid), dim3(512), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255,
