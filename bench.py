@@ -41,8 +41,12 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--batch", type=int, default=16,
-                   help="images per GPU per step (16: 6.6k images/s against 6.1k at 8, the per-step fixed costs amortised; 24-32 expose the serial host decisions)")
+    p.add_argument("--batch", type=int, default=64,
+                   help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64; "
+                        "the per-call fixed costs amortised, profiles/r02/batch_lanes.md)")
+    p.add_argument("--lanes", type=int, default=1,
+                   help="library lanes for the headline (phd_set_lanes); 1 keeps each kernel launch alone on "
+                        "the GPU, so its event duration prices the kernel (the roofline)")
     p.add_argument("--height", type=int, default=3000)
     p.add_argument("--width", type=int, default=4000)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -544,7 +548,7 @@ def config5(cx, total, iters=2):
     torch.cuda.empty_cache()
     return {"workload": f"{total} mixed-size RGB8 images (seed 5, {len(set(sizes_all))} sizes, "
                         f"{sum(h * w for h, w in sizes_all) / 1e6:.0f} Mpx) over {cx.world} GPU (LPT by pixels), "
-                        "full report, h/s/v 36/4/5, device-resident",
+                        f"full report, h/s/v 36/4/5, device-resident, {cx.lib.phd_set_lanes(0)} library lane(s)",
             "scaling": "strong", "n_gpus": cx.world,
             "images_per_s": round(m["images"] / m["elapsed"], 1),
             "megapixels_per_s": round(m["pixels"] / m["elapsed"] / 1e6, 1),
@@ -608,8 +612,25 @@ def main(argv=None):
     import photohive_dsp_amd  # noqa: F401
     cx = Ctx(args, world, rank, backend)
 
+    lib_lanes = cx.lib.phd_set_lanes(args.lanes)      # the library's setting, for the other configs
     hl = headline(cx)
     extra = {}
+    if not args.no_configs and args.lanes == 1:
+        # the same workload split over two library lanes (concurrent halves):
+        # more images/s, but each launch now shares the GPU, so its duration no
+        # longer prices the kernel alone
+        cx.lib.phd_set_lanes(2)
+        h2 = headline(cx)
+        cx.lib.phd_set_lanes(args.lanes)
+        m2 = h2["merged"]
+        extra["two_lanes"] = {
+            "workload": f"as the headline, each {args.batch}-image call split over 2 library lanes "
+                        "(phd_set_lanes(2): two contexts, the second on a library thread)",
+            "images_per_s": round(m2["images"] / m2["elapsed"], 1),
+            "ms_per_step": round(1000 * m2["elapsed"] / args.steps, 3),
+            "dominant_kernel": h2["dom"],
+            "avg_launch_us_shared": round(1000 * m2["kernel_ms"] / max(m2["launches"], 1), 2)}
+    cx.lib.phd_set_lanes(lib_lanes)
     if not args.no_configs:
         extra["config4"] = config4(cx, args.config4_images)
         extra["config5"] = config5(cx, args.config5_images)

@@ -243,6 +243,13 @@ int phd_last_timings(double* ms, int n);
 int phd_profile_kernels(unsigned mask);
 int phd_profile_read(int kernel, double* total_ms, long* launches);
 
+/* Lanes a device batch of >= 16 images on the library's stream is split over
+ * (1 or 2; default 2, or PHD_LANES).  Each lane is an independent context with
+ * its own streams and workspaces; the second runs on a library thread, so the
+ * two halves' kernels, host phases and launch gaps overlap.  Results do not
+ * depend on it.  lanes < 1 only queries.  Returns the previous setting. */
+int phd_set_lanes(int lanes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2,6 +2,7 @@
 // polar bin tables and grow-only workspaces.  One context per HIP device; a
 // mutex serialises calls that share it (the API itself keeps no globals per
 // call, unlike the reference's QUANTITY_WEIGHT / num_cores / FFTW state).
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -19,7 +20,7 @@ thread_local std::string g_error;
 thread_local double g_timings[8];
 thread_local int g_ntimings = 0;
 std::mutex g_ctx_mu;
-Context* g_ctx[64] = {};
+Context* g_ctx[64][kLanes] = {};
 }  // namespace
 
 void set_error(const std::string& msg) {
@@ -36,7 +37,9 @@ void record_timings(const double* ms, int n) {
     for (int i = 0; i < g_ntimings; i++) g_timings[i] = ms[i];
 }
 
-Context* get_context() {
+Context* get_context() { return get_context_lane(0); }
+
+Context* get_context_lane(int lane) {
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
         int n = 0;
@@ -51,7 +54,7 @@ Context* get_context() {
         }
     }
     std::lock_guard<std::mutex> lk(g_ctx_mu);
-    if (g_ctx[dev]) return g_ctx[dev];
+    if (g_ctx[dev][lane]) return g_ctx[dev][lane];
     auto* c = new Context();
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -90,8 +93,75 @@ Context* get_context() {
         delete c;
         return nullptr;
     }
-    g_ctx[dev] = c;
+    if (lane > 0 && g_ctx[dev][0]) c->prof.mask = g_ctx[dev][0]->prof.mask;   // profiled like lane 0
+    g_ctx[dev][lane] = c;
     return c;
+}
+
+// the contexts of this thread's device that exist (lane 0 first)
+std::vector<Context*> device_contexts() {
+    std::vector<Context*> out;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return out;
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    for (int l = 0; l < kLanes; l++)
+        if (g_ctx[dev][l]) out.push_back(g_ctx[dev][l]);
+    return out;
+}
+
+LaneWorker::LaneWorker() : th_([this] { loop(); }) {}
+
+void LaneWorker::run(std::function<void()> f) {
+    std::lock_guard<std::mutex> lk(m_);
+    job_ = std::move(f);
+    has_job_ = true;
+    cv_.notify_all();
+}
+
+void LaneWorker::wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [this] { return !has_job_; });
+}
+
+void LaneWorker::loop() {
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+        cv_.wait(lk, [this] { return has_job_; });
+        std::function<void()> f = std::move(job_);
+        lk.unlock();
+        f();
+        lk.lock();
+        has_job_ = false;
+        done_cv_.notify_all();
+    }
+}
+
+namespace {
+std::atomic<int> g_lanes{-1};
+}
+
+int lanes_setting() {
+    int l = g_lanes.load();
+    if (l < 0) {
+        const char* e = getenv("PHD_LANES");
+        l = e ? std::min(std::max(atoi(e), 1), kLanes) : kLanes;
+        g_lanes.store(l);
+    }
+    return l;
+}
+
+LaneWorker* lane_worker() {
+    // one per process (a forked child has none of its parent's threads)
+    static std::mutex m;
+    static LaneWorker* w = nullptr;
+    static pid_t owner = 0;
+    std::lock_guard<std::mutex> lk(m);
+    if (!w || owner != getpid()) {
+        w = new LaneWorker();   // never joined: it lives as long as the process
+        w->detach();
+        owner = getpid();
+    }
+    return w;
 }
 
 hipStream_t work_stream(Context* c, void* stream) {
@@ -390,26 +460,36 @@ const Context::Cls* get_cls(Context* c, const GridParams& gp) {
 
 }  // namespace phd
 
+extern "C" int phd_set_lanes(int lanes) {
+    const int prev = phd::lanes_setting();
+    if (lanes >= 1) phd::g_lanes.store(std::min(lanes, phd::kLanes));
+    return prev;
+}
+
 extern "C" int phd_profile_kernels(unsigned mask) {
-    phd::Context* c = phd::get_context();
-    if (!c) return -1;
-    std::lock_guard<std::mutex> lk(c->mu);
-    c->prof.mask = mask;
-    c->prof.calls = 0;
-    c->prof.pending.clear();
-    for (int k = 0; k < phd::kNumKernels; k++) {
-        c->prof.total_ms[k] = 0.0;
-        c->prof.launches[k] = 0;
+    if (!phd::get_context()) return -1;
+    for (phd::Context* c : phd::device_contexts()) {     // every lane of this device
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->prof.mask = mask;
+        c->prof.calls = 0;
+        c->prof.pending.clear();
+        for (int k = 0; k < phd::kNumKernels; k++) {
+            c->prof.total_ms[k] = 0.0;
+            c->prof.launches[k] = 0;
+        }
     }
     return 0;
 }
 
 extern "C" int phd_profile_read(int kernel, double* total_ms, long* launches) {
-    phd::Context* c = phd::get_context();
-    if (!c || kernel < 0 || kernel >= phd::kNumKernels) return -1;
-    std::lock_guard<std::mutex> lk(c->mu);
-    *total_ms = c->prof.total_ms[kernel];
-    *launches = c->prof.launches[kernel];
+    if (!phd::get_context() || kernel < 0 || kernel >= phd::kNumKernels) return -1;
+    *total_ms = 0.0;
+    *launches = 0;
+    for (phd::Context* c : phd::device_contexts()) {     // summed over the lanes
+        std::lock_guard<std::mutex> lk(c->mu);
+        *total_ms += c->prof.total_ms[kernel];
+        *launches += c->prof.launches[kernel];
+    }
     return 0;
 }
 

@@ -7,6 +7,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -209,7 +210,38 @@ struct Context {
     std::mutex mu;
 };
 // The context of the current HIP device (created on first use).  nullptr if no GPU.
+// Lanes: independent contexts of one device (own streams, workspaces and
+// tables).  A large device batch is split over them and the halves run
+// concurrently, so one half's host phases and launch gaps overlap the other's
+// kernels.  Lane 0 is the context every single call uses.
+constexpr int kLanes = 2;
 Context* get_context();
+Context* get_context_lane(int lane);
+std::vector<Context*> device_contexts();
+// A persistent thread that runs one job at a time (the second lane).
+class LaneWorker {
+public:
+    LaneWorker();
+    void run(std::function<void()> f);
+    void wait();
+    void detach() { th_.detach(); }
+    // one caller at a time owns the worker (run .. wait); a busy worker is
+    // not waited for: the caller runs its whole batch on lane 0 instead
+    bool try_acquire() { return user_mu_.try_lock(); }
+    void release() { user_mu_.unlock(); }
+
+private:
+    std::mutex user_mu_;
+    void loop();
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::function<void()> job_;
+    bool has_job_ = false;
+    std::thread th_;
+};
+LaneWorker* lane_worker();
+// lanes a large device batch is split over (PHD_LANES, default 2; phd_set_lanes)
+int lanes_setting();
 // The stream a call works on: the caller's, or (NULL) the library's own stream
 // ordered after every prior operation of the legacy null stream, so device
 // buffers a caller (or PyTorch's default stream) is still producing are

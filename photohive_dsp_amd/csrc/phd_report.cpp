@@ -12,6 +12,7 @@
 //
 // The FFT of an image depends only on K1's channel sums (for the DC bias), so
 // the host's palette decisions overlap the GPU's FFT work.
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -968,6 +969,45 @@ extern "C" void free_full_report(Full_Report_Data** report) {
     *report = nullptr;
 }
 
+// Runs body(context, lane, lanes) under the context's lock: on lane 0 (this
+// thread) only, or -- when `want`, lanes_setting() >= 2 and the lane worker is
+// free -- on lanes 0 and 1 concurrently, lane 1 (its own context, streams and
+// workspaces) on the lane worker thread.  An error of lane 1 is reported on
+// this thread unless lane 0 failed too.
+template <class F>
+static void on_lanes(Context* c0, bool want, F&& body) {
+    Context* c1 = nullptr;
+    if (want && lanes_setting() >= 2) {
+        c1 = get_context_lane(1);
+        if (!c1) clear_error();     // no second context: one lane
+    }
+    LaneWorker* lw = c1 ? lane_worker() : nullptr;
+    if (!lw || !lw->try_acquire()) {
+        std::lock_guard<std::mutex> lk(c0->mu);
+        body(c0, 0, 1);
+        return;
+    }
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::string err1;
+    lw->run([&] {
+        clear_error();
+        (void)hipSetDevice(dev);
+        {
+            std::lock_guard<std::mutex> lk1(c1->mu);
+            body(c1, 1, 2);
+        }
+        err1 = phd_last_error();
+    });
+    {
+        std::lock_guard<std::mutex> lk(c0->mu);
+        body(c0, 0, 2);
+    }
+    lw->wait();
+    lw->release();
+    if (!err1.empty() && std::string(phd_last_error()).empty()) set_error(err1);
+}
+
 extern "C" int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
                                        size_t image_stride, const phd_config* cfg, Full_Report_Data** out,
                                        int* status, void* stream) {
@@ -978,11 +1018,18 @@ extern "C" int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int h
     }
     Context* c = get_context();
     if (!c) return -1;
-    std::lock_guard<std::mutex> lk(c->mu);
     const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
     std::vector<const uint8_t*> imgs(n_images);
     for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
-    run_reports(c, imgs.data(), n_images, height, width, *cfg, nullptr, out, status, (hipStream_t)stream);
+    // two lanes for large batches on the library's streams: the second half on
+    // lane 1, so each half's host phases and launch gaps overlap the other's
+    // kernels
+    on_lanes(c, n_images >= 16 && !stream, [&](Context* cl, int lane, int nl) {
+        const int h = nl == 2 ? n_images / 2 : n_images;
+        const int i0 = lane ? h : 0, m = lane ? n_images - h : h;
+        run_reports(cl, imgs.data() + i0, m, height, width, *cfg, nullptr, out + i0, status + i0,
+                    (hipStream_t)stream);
+    });
     int fails = 0;
     for (int i = 0; i < n_images; i++) fails += status[i] != 0;
     return fails;
@@ -1175,22 +1222,28 @@ extern "C" int phd_report_batch_device_mixed(const uint8_t* const* d_images, con
     }
     Context* c = get_context();
     if (!c) return -1;
-    std::lock_guard<std::mutex> lk(c->mu);
-    int fails = 0;
-    for (const auto& grp : size_groups(heights, widths, n_images, 64)) {
-        const int m = (int)grp.size();
-        std::vector<const uint8_t*> ptrs(m);
-        std::vector<Full_Report_Data*> o(m, nullptr);
-        std::vector<int> st(m, -1);
-        for (int k = 0; k < m; k++) ptrs[k] = d_images[grp[k]];
-        run_reports(c, ptrs.data(), m, heights[grp[0]], widths[grp[0]], *cfg, nullptr, o.data(), st.data(),
-                    (hipStream_t)stream);
-        for (int k = 0; k < m; k++) {
-            out[grp[k]] = o[k];
-            status[grp[k]] = st[k];
-            fails += st[k] != 0;
+    const auto groups = size_groups(heights, widths, n_images, 64);
+    // the groups go to the lanes in order, each lane taking the next one when
+    // it is done with its last
+    std::atomic<size_t> next{0};
+    on_lanes(c, groups.size() >= 2 && !stream, [&](Context* cl, int, int) {
+        for (size_t gi; (gi = next.fetch_add(1)) < groups.size();) {
+            const auto& grp = groups[gi];
+            const int m = (int)grp.size();
+            std::vector<const uint8_t*> ptrs(m);
+            std::vector<Full_Report_Data*> o(m, nullptr);
+            std::vector<int> st(m, -1);
+            for (int k = 0; k < m; k++) ptrs[k] = d_images[grp[k]];
+            run_reports(cl, ptrs.data(), m, heights[grp[0]], widths[grp[0]], *cfg, nullptr, o.data(), st.data(),
+                        (hipStream_t)stream);
+            for (int k = 0; k < m; k++) {
+                out[grp[k]] = o[k];
+                status[grp[k]] = st[k];
+            }
         }
-    }
+    });
+    int fails = 0;
+    for (int i = 0; i < n_images; i++) fails += status[i] != 0;
     return fails;
 }
 

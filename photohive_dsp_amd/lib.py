@@ -83,6 +83,8 @@ lib.phd_profile_kernels.restype = ctypes.c_int
 lib.phd_profile_kernels.argtypes = [ctypes.c_uint]
 lib.phd_profile_read.restype = ctypes.c_int
 lib.phd_profile_read.argtypes = [ctypes.c_int, P(ctypes.c_double), P(ctypes.c_long)]
+lib.phd_set_lanes.restype = ctypes.c_int
+lib.phd_set_lanes.argtypes = [ctypes.c_int]
 KERNELS = ["hsv_stats", "fft_rows", "fft_cols", "palette_cutoffs", "palette_sums", "sharpness"]
 lib.phd_debug_time_kernel.restype = ctypes.c_int
 lib.phd_debug_time_kernel.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, P(PhdConfig),

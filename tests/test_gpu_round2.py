@@ -108,3 +108,34 @@ def test_host_batch_pipelined_groups_match_device_reports():
         assert r.color_palette.quantities == one.color_palette.quantities
         assert np.array_equal(_bins(r), _bins(one))
         assert [v.angle for v in r.blur_vectors] == [v.angle for v in one.blur_vectors]
+
+
+def test_two_lanes_match_one_lane():
+    """phd_set_lanes(2): a device batch of >= 16 images is split over two
+    contexts (the second half on the library's lane thread).  Every report
+    equals the one-lane report of the same batch, field by field, and a failing
+    second half would surface through the status array."""
+    phd, torch = _phd()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.lib import lib
+    imgs = [synth.make(("uniform", "structured", "hblur")[i % 3], 600, 800, 400 + i) for i in range(20)]
+    t = torch.from_numpy(np.stack(imgs)).cuda().contiguous()
+    prev = lib.phd_set_lanes(1)
+    try:
+        one = phd.report_device(t)
+        assert lib.phd_set_lanes(2) == 1
+        two = phd.report_device(t)
+        two_again = phd.report_device(t)
+    finally:
+        lib.phd_set_lanes(prev)
+    for a, b, c in zip(one, two, two_again):
+        for r in (b, c):
+            assert r.color_palette.group_ids == a.color_palette.group_ids
+            assert r.color_palette.quantities == a.color_palette.quantities
+            assert np.array_equal(_bins(r), _bins(a))
+            assert [(v.angle, v.magnitude) for v in r.blur_vectors] == \
+                [(v.angle, v.magnitude) for v in a.blur_vectors]
+            # fp64 sums from atomics: order-dependent in the last bits on either lane count
+            assert r.average_saturation == pytest.approx(a.average_saturation, rel=1e-12)
+            for f in ("Br", "Bg", "Bb", "Cr", "Cg", "Cb"):
+                assert getattr(r.rgb_stats, f) == pytest.approx(getattr(a.rgb_stats, f), rel=1e-12)
