@@ -40,7 +40,7 @@ def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=4)
     p.add_argument("--batch", type=int, default=64,
                    help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64; "
                         "the per-call fixed costs amortised, profiles/r02/batch_lanes.md)")
@@ -236,17 +236,24 @@ def headline(cx):
                                          status, None)
         if rc != 0:
             raise RuntimeError(f"report batch failed ({rc}): {cx.last_error()}")
-        for i in range(B):
-            lib.free_full_report(ctypes.byref(outs[i]))
+        lib.phd_free_reports(outs, B)
 
-    # warmup; the last warmup step with events on every kernel, to find the
-    # dominant one in steady state
+    # warmup, then one more step per kernel with events around that kernel's
+    # launches only (as in the timed region: events around every launch of all
+    # kernels shift time between them, and the row and column passes are
+    # within ~15 %), to find the dominant kernel in steady state
+    # The candidates are the three per-image passes (the palette tail runs once
+    # per step, ~0.2 ms); the last warmup steps are the profiled ones.
+    cand = [] if args.no_kernel_events else ["fft_cols", "fft_rows", "hsv_stats"][:max(1, args.warmup)]
     lib.phd_profile_kernels(0)
-    for _ in range(max(1, args.warmup) - 1):
+    for _ in range(max(1, args.warmup) - len(cand)):
         step()
-    lib.phd_profile_kernels(0 if args.no_kernel_events else (1 << len(KERNELS)) - 1)
-    step()
-    warm = kernel_times(lib, KERNELS)
+    warm = {}
+    for name in cand:
+        lib.phd_profile_kernels(1 << KERNELS.index(name))
+        step()
+        warm.update({n: v for n, v in kernel_times(lib, KERNELS).items() if n == name})
+    nprof = 1
     dom = max(warm, key=lambda k: warm[k]["total_ms"]) if warm else None
     # timed region: HIP events (recorded by the launches themselves, on the
     # stream the kernel runs on) bracket every launch of the dominant kernel in
@@ -271,7 +278,7 @@ def headline(cx):
     m = cx.merge(elapsed, n_img, n_img * H * W, n_img * algorithmic_bytes("report", H, W), km, kl)
     del d_imgs
     torch.cuda.empty_cache()
-    res = {"merged": m, "dom": dom, "warm": warm, "kern": kern,
+    res = {"merged": m, "dom": dom, "warm": warm, "warm_steps": nprof, "kern": kern,
            "stages": {k: stage[j] / args.steps for j, k in enumerate(
                ("hsv_stats", "fft_rows_cols", "palette_pass2", "gpu_total", "host_total", "host_enqueue",
                 "host_decisions", "host_assembly"))}}
@@ -379,8 +386,7 @@ def host_buffers(cx, h=3000, w=4000, n=64, iters=3):
     def run():
         if lib.phd_report_batch_u8(ptrs, hs, ws, n, ctypes.byref(cfg), outs, st) != 0:
             raise RuntimeError(cx.last_error())
-        for i in range(n):
-            lib.free_full_report(ctypes.byref(outs[i]))
+        lib.phd_free_reports(outs, n)
     run()
     t0 = time.perf_counter()
     for _ in range(iters):
@@ -532,8 +538,7 @@ def config5(cx, total, iters=2):
     def run():
         if lib.phd_report_batch_device_mixed(ptrs, hs, ws, n, ctypes.byref(cfg), outs, st, None) != 0:
             raise RuntimeError(f"mixed batch failed: {cx.last_error()}")
-        for i in range(n):
-            lib.free_full_report(ctypes.byref(outs[i]))
+        lib.phd_free_reports(outs, n)
     run()
     cx.barrier()
     t0 = time.perf_counter()
@@ -667,7 +672,7 @@ def main(argv=None):
         if dom in kern:
             # the palette passes take the whole batch in one launch, the FFT passes one image
             # (from the last warmup step, whose every launch was bracketed)
-            per_launch = B / warm[dom]["launches"]
+            per_launch = hl["warm_steps"] * B / warm[dom]["launches"]
             ab = algorithmic_bytes(dom, H, W) * per_launch
             # every rank's sampled launches of the dominant kernel (counter all-gather)
             avg_us = 1000 * m["kernel_ms"] / max(m["launches"], 1)

@@ -105,6 +105,8 @@ Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundaries* salien
 /* Replaces free_full_report, src/interface.c:97-111: frees the whole tree and
  * sets *report = NULL. */
 void free_full_report(Full_Report_Data** report);
+/* free_full_report over an array of n reports (a batch call's `out`); NULL entries are skipped. */
+void phd_free_reports(Full_Report_Data** reports, int n);
 
 /* Replaces get_blur_profile_visual, src/blur_profile.c:140-180 (bound by
  * /root/reference/lib.py:36-37).  Caller owns the result (free with

@@ -353,9 +353,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     }
     if (!precheck(height, width) || !check_crops(crops, height, width)) return false;
     const hipStream_t st = work_stream(c, stream);
+    // ev_img_fft only orders the download stream after a column pass on this
+    // device: no system-scope fence (PHD_EV_FENCE=1: the default event)
+    static const bool fence = getenv("PHD_EV_FENCE") != nullptr;
     while ((int)c->ev_img_fft.size() < n) {
         hipEvent_t a, b;
-        PHD_HIP(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+        PHD_HIP(hipEventCreateWithFlags(&a, fence ? hipEventDisableTiming : hipEventDisableSystemFence));
         PHD_HIP(hipEventCreateWithFlags(&b, hipEventDisableTiming));
         c->ev_img_fft.push_back(a);
         c->ev_img_dl.push_back(b);
@@ -939,6 +942,10 @@ extern "C" Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundar
     if (!c) return nullptr;
     std::lock_guard<std::mutex> lk(c->mu);
     return report_planar(c, image->r, image->g, image->b, image->height, image->width, cfg, crops);
+}
+
+extern "C" void phd_free_reports(Full_Report_Data** reports, int n) {
+    for (int i = 0; reports && i < n; i++) free_full_report(&reports[i]);
 }
 
 extern "C" void free_full_report(Full_Report_Data** report) {

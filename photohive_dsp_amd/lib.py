@@ -95,6 +95,8 @@ lib.phd_debug_gfft.restype = ctypes.c_int
 lib.phd_debug_gfft.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_long]
 lib.free_full_report.restype = None
 lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
+lib.phd_free_reports.restype = None
+lib.phd_free_reports.argtypes = [P(P(Full_Report_Data)), ctypes.c_int]
 lib.phd_free_pgm.argtypes = [P(Image_PGM)]
 lib.phd_last_error.restype = ctypes.c_char_p
 lib.phd_device_info.restype = ctypes.c_int
