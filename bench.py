@@ -45,8 +45,12 @@ def parse(argv=None):
                    help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64; "
                         "the per-call fixed costs amortised, profiles/r02/batch_lanes.md)")
     p.add_argument("--lanes", type=int, default=1,
-                   help="library lanes for the headline (phd_set_lanes); 1 keeps each kernel launch alone on "
-                        "the GPU, so its event duration prices the kernel (the roofline)")
+                   help="library lanes for every config of the run (phd_set_lanes); 1 keeps each kernel launch "
+                        "alone on the GPU, so its event duration prices the kernel (the roofline)")
+    p.add_argument("--two-lanes", action="store_true",
+                   help="also run the headline workload over two library lanes (phd_set_lanes(2)) and report its "
+                        "images/s as two_lanes; off by default, so that every kernel launch of the default command "
+                        "runs alone and its rocprofv3 statistics agree with the roofline")
     p.add_argument("--height", type=int, default=3000)
     p.add_argument("--width", type=int, default=4000)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -617,10 +621,10 @@ def main(argv=None):
     import photohive_dsp_amd  # noqa: F401
     cx = Ctx(args, world, rank, backend)
 
-    lib_lanes = cx.lib.phd_set_lanes(args.lanes)      # the library's setting, for the other configs
+    cx.lib.phd_set_lanes(args.lanes)                  # every config of this run
     hl = headline(cx)
     extra = {}
-    if not args.no_configs and args.lanes == 1:
+    if args.two_lanes and args.lanes == 1:
         # the same workload split over two library lanes (concurrent halves):
         # more images/s, but each launch now shares the GPU, so its duration no
         # longer prices the kernel alone
@@ -635,7 +639,6 @@ def main(argv=None):
             "ms_per_step": round(1000 * m2["elapsed"] / args.steps, 3),
             "dominant_kernel": h2["dom"],
             "avg_launch_us_shared": round(1000 * m2["kernel_ms"] / max(m2["launches"], 1), 2)}
-    cx.lib.phd_set_lanes(lib_lanes)
     if not args.no_configs:
         extra["config4"] = config4(cx, args.config4_images)
         extra["config5"] = config5(cx, args.config5_images)
