@@ -90,3 +90,22 @@ def test_reference_rejections_are_null_before_touching_gpu():
         with pytest.raises(ValueError):
             phd.get_report(np.zeros((h, w, 3), np.uint8))
         assert "350" in last_error() or "aspect" in last_error()
+
+
+def test_lanes_setting_and_batch_free_need_no_gpu():
+    """phd_set_lanes clamps to 1..2 and lanes < 1 only query; phd_free_reports
+    skips NULL entries and leaves every entry NULL (host-only calls)."""
+    from photohive_dsp_amd.lib import lib
+    from photohive_dsp_amd.structures import Full_Report_Data
+    prev = lib.phd_set_lanes(0)
+    assert prev in (1, 2)
+    try:
+        assert lib.phd_set_lanes(1) == prev
+        assert lib.phd_set_lanes(7) == 1
+        assert lib.phd_set_lanes(0) == 2
+    finally:
+        lib.phd_set_lanes(prev)
+    outs = (ctypes.POINTER(Full_Report_Data) * 3)()
+    lib.phd_free_reports(outs, 3)
+    lib.phd_free_reports(None, 0)
+    assert all(not outs[i] for i in range(3))
