@@ -75,20 +75,24 @@ Context* get_context_lane(int lane) {
     // idle GPU when recorded before a download)
     for (int i = 0; i < 8; i++)
         (void)hipEventCreateWithFlags(&c->ev[i], (i == 4 || i == 5) ? hipEventDefault : hipEventDisableSystemFence);
+    // the events that only order one device stream after another: no
+    // system-scope fence either (each fenced record left the GPU idle ~5.7 us
+    // between two kernels; PHD_EV_FENCE=1 restores it)
+    const unsigned of = device_event_flags();
     if (hipStreamCreateWithFlags(&c->tail, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_k1, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_dl_sd, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_k1, of) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_tail, of) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_dl_sd, of) != hipSuccess ||
         hipStreamCreateWithFlags(&c->fft, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_ws, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fft, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ws, of) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fft, of) != hipSuccess ||
         hipStreamCreateWithFlags(&c->fft2, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->dl, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_rows[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_rows[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_cols[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_cols[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_null, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_rows[0], of) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rows[1], of) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_cols[0], of) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_cols[1], of) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_null, of) != hipSuccess) {
         set_error("hipStreamCreate failed");
         delete c;
         return nullptr;
@@ -96,6 +100,11 @@ Context* get_context_lane(int lane) {
     if (lane > 0 && g_ctx[dev][0]) c->prof.mask = g_ctx[dev][0]->prof.mask;   // profiled like lane 0
     g_ctx[dev][lane] = c;
     return c;
+}
+
+unsigned device_event_flags() {
+    static const bool fence = getenv("PHD_EV_FENCE") != nullptr;
+    return fence ? hipEventDisableTiming : hipEventDisableSystemFence;
 }
 
 // the contexts of this thread's device that exist (lane 0 first)

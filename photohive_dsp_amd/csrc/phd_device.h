@@ -28,7 +28,7 @@ namespace phd {
 template <typename F, typename... Args>
 inline void phd_launch(F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
     LaunchEvents& e = launch_events();
-    const bool timed = e.start != nullptr && !e.used;
+    const bool timed = (e.start != nullptr || e.stop != nullptr) && !e.used;
     hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, timed ? e.start : nullptr,
                           timed ? e.stop : nullptr, 0u, args...);
     if (timed) e.used = true;

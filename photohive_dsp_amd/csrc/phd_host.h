@@ -217,6 +217,9 @@ struct Context {
 constexpr int kLanes = 2;
 Context* get_context();
 Context* get_context_lane(int lane);
+// flags of the events that only order device streams (no system-scope fence
+// unless PHD_EV_FENCE is set; timing enabled, so a launch can record them)
+unsigned device_event_flags();
 std::vector<Context*> device_contexts();
 // A persistent thread that runs one job at a time (the second lane).
 class LaneWorker {

@@ -354,11 +354,10 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (!precheck(height, width) || !check_crops(crops, height, width)) return false;
     const hipStream_t st = work_stream(c, stream);
     // ev_img_fft only orders the download stream after a column pass on this
-    // device: no system-scope fence (PHD_EV_FENCE=1: the default event)
-    static const bool fence = getenv("PHD_EV_FENCE") != nullptr;
+    // device (device_event_flags: no system-scope fence)
     while ((int)c->ev_img_fft.size() < n) {
         hipEvent_t a, b;
-        PHD_HIP(hipEventCreateWithFlags(&a, fence ? hipEventDisableTiming : hipEventDisableSystemFence));
+        PHD_HIP(hipEventCreateWithFlags(&a, device_event_flags()));
         PHD_HIP(hipEventCreateWithFlags(&b, hipEventDisableTiming));
         c->ev_img_fft.push_back(a);
         c->ev_img_dl.push_back(b);
@@ -523,8 +522,17 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             auto* bins = (unsigned long long*)(dw + L.C(n, i) + L.c_bins);
             double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
             const int ps = c->prof.begin(kFftCols, sf);
+            // an unprofiled column pass that ends a download group records the
+            // group's event itself (its completion signal): a separate event
+            // record between two kernels leaves the GPU idle ~4 us
+            // (compile-time plans only: one launch is the whole column pass)
+            const bool own = fs.ct && ps < 0 && dl_end(i) && !ncrops &&
+                             device_event_flags() == hipEventDisableSystemFence;
+            if (own) launch_events() = LaunchEvents{nullptr, c->ev_img_fft[i], false};
             PHD_HIP(launch_cols_sel(fs, c->d_inter + (size_t)(i - g0) * inter_elems, height, width, wf, tbl->d_map,
                                     nbins, bins, fmx, sums, nullptr, sf));
+            const bool recorded = own && launch_events().used;
+            if (own) launch_events() = LaunchEvents{};
             c->prof.end(ps, sf);
             if (ncrops) {
                 // crop boxes: sharpness on the full-resolution luma before DC removal
@@ -533,7 +541,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                                          crop_arr.data() + 3 * ncrops, c->d_k255,
                                          (double*)(dw + L.C(n, i) + L.c_sharp), sf));
             }
-            if (dl_end(i)) PHD_HIP(hipEventRecord(c->ev_img_fft[i], sf));
+            if (dl_end(i) && !recorded) PHD_HIP(hipEventRecord(c->ev_img_fft[i], sf));
         }
     }
     // the last column pass ends the FFT work (it waited for the last row pass)
