@@ -431,12 +431,27 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
 
     PHD_HIP(hipMemsetAsync(dw, 0, (size_t)n * (L.a_bytes + L.c_bytes), st));
     PHD_HIP(hipEventRecord(c->ev_ws, st));
-    PHD_HIP(hipEventRecord(c->ev[0], st));
-    if (!launch_k1(c, L, n, d_imgs, height, width, ds, gp, cls, nchunks, fused, st)) return false;
-    PHD_HIP(hipEventRecord(c->ev[1], st));
-    PHD_HIP(hipEventRecord(c->ev_k1, st));
-    PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, st));
-    PHD_HIP(hipEventRecord(c->ev[5], st));
+    // An unprofiled one-launch K1 records its stage events with its own
+    // dispatch and completion (no marker packets between it and the first row
+    // pass), and ev[1] then stands for ev_k1; the A records go down on the
+    // download stream, beside the FFTs instead of ahead of them.
+    static const bool k1_events_off = getenv("PHD_K1_MARKERS") != nullptr;
+    const bool k1_own = ds <= 1 && !(c->prof.mask & (1u << kK1)) && !k1_events_off &&
+                        device_event_flags() == hipEventDisableSystemFence;
+    if (k1_own) launch_events() = LaunchEvents{c->ev[0], c->ev[1], false};
+    else PHD_HIP(hipEventRecord(c->ev[0], st));
+    const bool k1_ok = launch_k1(c, L, n, d_imgs, height, width, ds, gp, cls, nchunks, fused, st);
+    const bool k1_rec = k1_own && launch_events().used;
+    if (k1_own) launch_events() = LaunchEvents{};
+    if (!k1_ok) return false;
+    if (k1_own && !k1_rec) PHD_HIP(hipEventRecord(c->ev[0], st));   // (a K1 path without phd_launch: timing only)
+    if (!k1_rec) PHD_HIP(hipEventRecord(c->ev[1], st));
+    const hipEvent_t ev_k1 = k1_rec ? c->ev[1] : c->ev_k1;
+    if (!k1_rec) PHD_HIP(hipEventRecord(c->ev_k1, st));
+    const hipStream_t sa = k1_rec ? c->dl : st;
+    if (sa != st) PHD_HIP(hipStreamWaitEvent(sa, ev_k1, 0));
+    PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, sa));
+    PHD_HIP(hipEventRecord(c->ev[5], sa));
     // PHD_FFT_OVERLAP=1 (compile-time plans): the row pass sums the channels
     // itself (the column pass's DC bias), so the FFT chain needs nothing from
     // K1 and runs beside it on its own stream.  Measured slower (5.75k vs 6.05k
@@ -449,12 +464,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const hipStream_t sf = (pipe || own_dc) ? c->fft : st;
     if (sf != st) {
         PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
-        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sf, ev_k1, 0));
     }
     const size_t inter_elems = inter_one / sizeof(double2);
     const hipStream_t sc = c->fft2;
     if (pipe) {
-        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sc, c->ev_k1, 0));   // DC removal needs K1's sums
+        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sc, ev_k1, 0));   // DC removal needs K1's sums
         PHD_HIP(hipStreamWaitEvent(sc, c->ev_ws, 0));
         for (int i = 0; i < n; i++) {
             const int b = i & 1;
@@ -515,7 +530,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                                     c->d_inter + (size_t)(i - g0) * inter_elems, sf, rsum));
             c->prof.end(ps, sf);
         }
-        if (g0 == 0 && fs.ct && !own_dc && sf != st) PHD_HIP(hipStreamWaitEvent(sf, c->ev_k1, 0));
+        if (g0 == 0 && fs.ct && !own_dc && sf != st) PHD_HIP(hipStreamWaitEvent(sf, ev_k1, 0));
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = own_dc ? (const unsigned long long*)(dw + L.C(n, i) + L.c_rsum)
                                                     : (const unsigned long long*)(dw + L.A(i) + L.a_sums);
@@ -608,7 +623,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     }
     // the second pass on the tail stream, after K1, concurrent with the FFTs
     const hipStream_t s2 = c->tail;
-    PHD_HIP(hipStreamWaitEvent(s2, c->ev_k1, 0));
+    PHD_HIP(hipStreamWaitEvent(s2, ev_k1, 0));
     uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
     const bool batched = ds <= 1 && (fused || palette_sums_b_lds(gp.tl, max_slots) <= 160 * 1024);
     // the B records (and, batched, the Kcut list right after them): one copy
