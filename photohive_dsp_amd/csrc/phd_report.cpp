@@ -195,7 +195,7 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
     // bins[angle][radius] as the reference's row pointers, the rows in one
     // block (free_full_report frees bins[0] and the pointer array)
     bp->bins = (Bin**)malloc(sizeof(Bin*) * na);
-    Bin* rows = (Bin*)calloc((size_t)na * nr > 0 ? (size_t)na * nr : 1, sizeof(Bin));
+    Bin* rows = (Bin*)malloc(sizeof(Bin) * ((size_t)na * nr > 0 ? (size_t)na * nr : 1));   // finish_blur writes every bin
     for (int a = 0; a < na; a++) bp->bins[a] = rows + (size_t)a * nr;
     Blur_Vector_Group* bv = (Blur_Vector_Group*)calloc(1, sizeof(Blur_Vector_Group));
     bv->len_vectors = 10;
