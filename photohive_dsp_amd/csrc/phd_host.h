@@ -200,6 +200,8 @@ struct Context {
     // host-buffer uploads (phd_upload.cpp): pinned slot ring on the h2d stream,
     // two device staging buffers for overlapping groups
     hipStream_t h2d = nullptr;
+    hipStream_t h2d2 = nullptr;     // second upload stream (every other image of a group)
+    hipEvent_t ev_h2d2 = nullptr;
     uint8_t* h2d_slots = nullptr;
     std::vector<hipEvent_t> ev_slot;
     std::vector<char> slot_used;
@@ -330,6 +332,10 @@ void record_timings(const double* ms, int n);
 bool upload_init(Context* c);
 // Copy `bytes` host bytes to d_dst through the pinned slot ring on c->h2d.  On
 // return the caller's buffer has been read; the DMA may still run.
-bool upload_async(Context* c, uint8_t* d_dst, const uint8_t* src, size_t bytes, std::string* why);
+bool upload_async(Context* c, uint8_t* d_dst, const uint8_t* src, size_t bytes, std::string* why,
+                  hipStream_t s = nullptr);
+// 2 (default, PHD_UPLOAD_STREAMS): a group's images alternate between the h2d
+// and h2d2 streams, each fed by its own host thread (runtime pageable path only)
+int upload_streams();
 
 }  // namespace phd

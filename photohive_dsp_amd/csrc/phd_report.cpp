@@ -1301,7 +1301,8 @@ extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heig
     std::lock_guard<std::mutex> lk(c->mu);
     if (!upload_init(c)) return -1;
     std::vector<std::vector<int>> groups;
-    for (auto& g : size_groups(heights, widths, n_images, 16)) {
+    static const int gcap = getenv("PHD_HOST_GROUP") ? std::max(1, atoi(getenv("PHD_HOST_GROUP"))) : 16;
+    for (auto& g : size_groups(heights, widths, n_images, gcap)) {
         if (precheck(heights[g[0]], widths[g[0]])) groups.push_back(std::move(g));
     }
     int fails = 0;
@@ -1316,8 +1317,26 @@ extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heig
     };
     auto upload = [c, images, heights, widths](const std::vector<int>& g, int b, Up* u) {
         const size_t bytes = 3 * (size_t)widths[g[0]] * heights[g[0]];
-        for (size_t k = 0; k < g.size() && u->ok; k++)
-            u->ok = upload_async(c, c->d_stage2[b] + k * bytes, images[g[k]], bytes, &u->why);
+        if (upload_streams() == 2 && g.size() > 1) {
+            // odd images on h2d2 from a second thread: two pageable copies in flight
+            Up u2;
+            std::thread t2([&] {
+                for (size_t k = 1; k < g.size() && u2.ok; k += 2)
+                    u2.ok = upload_async(c, c->d_stage2[b] + k * bytes, images[g[k]], bytes, &u2.why, c->h2d2);
+            });
+            for (size_t k = 0; k < g.size() && u->ok; k += 2)
+                u->ok = upload_async(c, c->d_stage2[b] + k * bytes, images[g[k]], bytes, &u->why, c->h2d);
+            t2.join();
+            if (u->ok && !u2.ok) *u = u2;
+            if (u->ok && (hipEventRecord(c->ev_h2d2, c->h2d2) != hipSuccess ||
+                          hipStreamWaitEvent(c->h2d, c->ev_h2d2, 0) != hipSuccess)) {
+                u->ok = false;
+                u->why = "upload event failed";
+            }
+        } else {
+            for (size_t k = 0; k < g.size() && u->ok; k++)
+                u->ok = upload_async(c, c->d_stage2[b] + k * bytes, images[g[k]], bytes, &u->why);
+        }
         if (u->ok && hipEventRecord(c->ev_up[b], c->h2d) != hipSuccess) {
             u->ok = false;
             u->why = "upload event failed";
@@ -1350,6 +1369,7 @@ extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heig
     if (th.joinable()) th.join();
     // the caller's buffers may be freed on return: every transfer has completed
     (void)hipStreamSynchronize(c->h2d);
+    (void)hipStreamSynchronize(c->h2d2);
     (void)hipStreamSynchronize(c->stream);
     for (int i = 0; i < n_images; i++) fails += status[i] != 0;
     return fails;
