@@ -334,8 +334,8 @@ bool upload_init(Context* c);
 // return the caller's buffer has been read; the DMA may still run.
 bool upload_async(Context* c, uint8_t* d_dst, const uint8_t* src, size_t bytes, std::string* why,
                   hipStream_t s = nullptr);
-// 2 (default, PHD_UPLOAD_STREAMS): a group's images alternate between the h2d
-// and h2d2 streams, each fed by its own host thread (runtime pageable path only)
+// 2 (PHD_UPLOAD_STREAMS=2; default 1): a group's images alternate between the
+// h2d and h2d2 streams, each fed by its own host thread (runtime pageable path only)
 int upload_streams();
 
 }  // namespace phd

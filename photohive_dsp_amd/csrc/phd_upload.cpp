@@ -11,10 +11,11 @@
 //
 // phd_report_batch_u8 runs the uploads of the next same-size group on an
 // uploader thread while the current group's reports compute (two device
-// staging buffers), so the H2D traffic overlaps the GPU work.  The group's
-// odd images go up on a second stream from a second thread (two pageable
-// copies in flight: 1442-1453 against 1386-1439 images/s, medians of 7
-// batches; PHD_UPLOAD_STREAMS=1 for one).
+// staging buffers), so the H2D traffic overlaps the GPU work.
+// PHD_UPLOAD_STREAMS=2 sends a group's odd images on a second stream from a
+// second thread (two pageable copies in flight): 1442-1453 against 1386-1439
+// images/s alone (tools/host_overlap.py), but 860-909 against 1375-1414 in
+// bench.py's host_buffer leg, so one stream is the default.
 #include <algorithm>
 #include <cstring>
 #include <thread>
@@ -72,7 +73,7 @@ static bool staged_upload() {
 
 int upload_streams() {
     static const int n = getenv("PHD_UPLOAD_STREAMS") ? std::min(2, std::max(1, atoi(getenv("PHD_UPLOAD_STREAMS"))))
-                                                      : 2;
+                                                      : 1;
     return staged_upload() ? 1 : n;
 }
 
