@@ -139,3 +139,41 @@ def test_two_lanes_match_one_lane():
             assert r.average_saturation == pytest.approx(a.average_saturation, rel=1e-12)
             for f in ("Br", "Bg", "Bb", "Cr", "Cg", "Cb"):
                 assert getattr(r.rgb_stats, f) == pytest.approx(getattr(a.rgb_stats, f), rel=1e-12)
+
+
+def test_concurrent_callers_with_lanes():
+    """Two host threads call report_device at once with 16-image batches (lanes
+    on): one gets the lane worker, the other runs its whole batch on lane 0
+    (the worker is never waited for); no deadlock, and every report equals the
+    one-lane report of its image."""
+    import threading
+    phd, torch = _phd()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.lib import lib
+    imgs = [synth.make(("uniform", "structured")[i % 2], 480, 640, 700 + i) for i in range(16)]
+    t = torch.from_numpy(np.stack(imgs)).cuda().contiguous()
+    prev = lib.phd_set_lanes(1)
+    try:
+        ref = phd.report_device(t)
+        lib.phd_set_lanes(2)
+        out, errs = [None, None], []
+
+        def work(k):
+            try:
+                out[k] = phd.report_device(t)
+            except Exception as e:        # surfaced below
+                errs.append(e)
+        th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=60)
+        assert not any(x.is_alive() for x in th), "a caller is stuck"
+        assert not errs, errs
+    finally:
+        lib.phd_set_lanes(prev)
+    for reps in out:
+        for a, r in zip(ref, reps):
+            assert r.color_palette.group_ids == a.color_palette.group_ids
+            assert r.color_palette.quantities == a.color_palette.quantities
+            assert np.array_equal(_bins(r), _bins(a))
