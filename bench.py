@@ -39,7 +39,7 @@ METRIC = "images/sec (4000×3000 RGB8 full report) at 1/2/4/8 GPUs; HBM GB/s vs 
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=4)
     p.add_argument("--batch", type=int, default=64,
                    help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64; "
