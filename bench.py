@@ -55,7 +55,8 @@ def parse(argv=None):
     p.add_argument("--width", type=int, default=4000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-procs", type=int, default=0,
-                   help="CPU baseline processes (0: the cores this process may use, at most 16)")
+                   help="CPU baseline processes (0: the affinity set, bounded by the cgroup quota and the box's "
+                        "per-GPU CPU share; cpu_topology)")
     p.add_argument("--no-kernel-events", action="store_true",
                    help="do not bracket kernels with HIP events (roofline then null)")
     p.add_argument("--no-configs", "--no-config3", dest="no_configs", action="store_true",
@@ -112,6 +113,59 @@ def _fft_engine():
     return eng + ("" if fftw is None else f"; libfftw3 present ({fftw}) but not used")
 
 
+def _cgroup_cpu_max():
+    """The cgroup v2 CPU quota of this process ("max 100000" = none), or None."""
+    for p in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(p) as f:
+                return f.read().strip()
+        except OSError:
+            pass
+    try:                                                   # cgroup v1
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = f.read().strip()
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            return f"{'max' if q == '-1' else q} {f.read().strip()}"
+    except OSError:
+        return None
+
+
+def _physical_cores(cpus):
+    """Distinct physical cores among the logical CPUs `cpus` (SMT siblings once)."""
+    seen = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                seen.add(f.read().strip())
+        except OSError:
+            seen.add(str(c))
+    return len(seen)
+
+
+def cpu_topology():
+    """What this process may run on (P = the host's CPUs), and the
+    process count the baseline uses: the affinity set, bounded by the cgroup quota
+    and by the CPU share the GPU box grants one GPU's job (OMP_NUM_THREADS there:
+    worker pools are to be sized to it), with the reason recorded."""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = _cgroup_cpu_max()
+    quota_cpus = None
+    if quota and not quota.startswith("max"):
+        q, per = quota.split()[:2]
+        quota_cpus = max(1, -(-int(q) // int(per)))
+    share = os.environ.get("OMP_NUM_THREADS")
+    share = int(share) if share and share.isdigit() and int(share) > 0 else None
+    procs, why = len(aff), "every CPU in sched_getaffinity"
+    if quota_cpus is not None and quota_cpus < procs:
+        procs, why = quota_cpus, f"cgroup cpu.max quota {quota} allows {quota_cpus} CPUs"
+    if share is not None and share < procs:
+        procs, why = share, (f"the GPU box grants one GPU's job a share of {share} CPUs (OMP_NUM_THREADS={share}; "
+                             f"its rules size worker pools to that share), of {len(aff)} in the affinity set")
+    return {"affinity_cpus": len(aff), "affinity_physical_cores": _physical_cores(aff),
+            "host_cpus_online": os.sysconf("SC_NPROCESSORS_ONLN"), "cgroup_cpu_max": quota,
+            "cpu_share_env": share, "procs": procs, "procs_reason": why}
+
+
 def _cpu_worker(job):
     """One baseline process: the oracle build `opt` on its own images."""
     opt, h, w, seeds, start_at, fft_workers = job
@@ -128,20 +182,31 @@ def _cpu_worker(job):
     return len(imgs), t0, time.time()
 
 
-def cpu_baseline(h, w, procs):
+def _throughput(h, w, procs, per, seed0):
+    """`procs` processes, `per` images each, common start: (images, wall s)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        start_at = time.time() + 5.0 + 0.2 * procs
+        jobs = [("O2", h, w, [seed0 + per * p + k for k in range(per)], start_at, 1) for p in range(procs)]
+        res = pool.map(_cpu_worker, jobs, chunksize=1)
+    return sum(r[0] for r in res), max(r[2] for r in res) - min(r[1] for r in res)
+
+
+def cpu_baseline(h, w, topo, procs):
     """BASELINE.md 3 / SURVEY.md 8(d): the C restatement of the reference path
     (oracle/phd_oracle.c + scipy rfft2 for FFTW), u8 host buffer -> full report,
     on this host's cores.  Throughput mode (the `value`): `procs` independent
-    processes (the reference is not reentrant), one image at a time each, -O2.
+    processes (the reference is not reentrant), one image at a time each, -O2;
+    the same at half the processes shows whether the rate scales with cores.
     Latency mode: one image at a time with the FFT on `procs` threads (the
-    reference plans FFTW with num_cores threads), at -O2 and at -O0 (the
+    reference plans FFTW with sysconf(_SC_NPROCESSORS_ONLN) threads,
+    src/utilities.c:128, src/fft_processing.c:21), at -O2 and at -O0 (the
     reference ships -O0)."""
-    import multiprocessing as mp
     from oracle import oracle as orc
     from photohive_dsp_amd import synth
     orc.build()                                            # liboracle.so + liboracle_O0.so (no-op when built)
-    out = {"unit": "images/s", "kind": "port", "cores": procs,
-           "host_cpus_online": os.sysconf("SC_NPROCESSORS_ONLN"), "cpu_model": _cpu_model(),
+    out = {"unit": "images/s", "kind": "port", "cores": procs, **topo, "cpu_model": _cpu_model(),
            "fft_engine": _fft_engine()}
     # latency mode: one image at a time, FFT on all `procs` cores
     lat = {}
@@ -155,22 +220,43 @@ def cpu_baseline(h, w, procs):
         dt = time.perf_counter() - t0
         lat[opt] = {"ms_per_image": round(1000 * dt / n, 1), "images_per_s": round(n / dt, 3),
                     "sample": f"{n} x {h}x{w} uniform, one at a time"}
+    # BASELINE config 1: one 1024x1024 uniform image (splitmix64 seed 20241125,
+    # tests/golden/uniform_1024.npz pins the report), one call at a time
+    c1 = {}
+    img1 = synth.uniform(1024, 1024, 20241125)
+    for opt in ("O2", "O0"):
+        orc.use_build(opt)
+        orc.report(img1, fft_workers=procs)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            orc.report(img1, fft_workers=procs)
+            ts.append(time.perf_counter() - t0)
+        c1[f"ms_{opt}"] = round(1000 * sorted(ts)[1], 2)
+    out["config1"] = {"workload": "1 x 1024x1024 uniform RGB8 (seed 20241125), full report, median of 3", **c1}
     orc.use_build("O2")
-    # throughput mode: `procs` processes, 2 images each, common start
+    # throughput mode: `procs` processes, 2 images each, common start; then half
+    # as many processes (does the rate scale with the cores used?)
     per = 2
-    ctx = mp.get_context("spawn")
-    with ctx.Pool(procs) as pool:
-        start_at = time.time() + 5.0 + 0.2 * procs
-        jobs = [("O2", h, w, [30_000 + per * p + k for k in range(per)], start_at, 1) for p in range(procs)]
-        res = pool.map(_cpu_worker, jobs, chunksize=1)
-    n_img = sum(r[0] for r in res)
-    wall = max(r[2] for r in res) - min(r[1] for r in res)
+    n_img, wall = _throughput(h, w, procs, per, 30_000)
     out["value"] = round(n_img / wall, 3)
     out["mode"] = "throughput"
+    out["per_core_images_per_s"] = round(n_img / wall / procs, 4)
     out["sample"] = (f"{procs} processes x {per} x {h}x{w} uniform RGB8 full reports (-O2 restatement, "
                      f"1 FFT thread each): {n_img} images in {wall:.1f} s wall")
+    half = max(1, procs // 2)
+    n_h, wall_h = _throughput(h, w, half, per, 40_000)
+    scal = (n_img / wall) / (n_h / wall_h) / (procs / half) if half < procs else 1.0
     out["modes"] = {"throughput_O2": {"images_per_s": out["value"], "processes": procs},
+                    f"throughput_O2_{half}_procs": {"images_per_s": round(n_h / wall_h, 3), "processes": half},
+                    "scaling_efficiency_half_to_full": round(scal, 3),
                     "latency_O2": lat["O2"], "latency_O0": lat["O0"]}
+    # what the whole affinity set would give if the per-core rate held (a
+    # projection, not a measurement: more processes than the granted share are
+    # not run on the shared box)
+    out["projected_affinity_images_per_s"] = round(out["per_core_images_per_s"] * topo["affinity_physical_cores"], 2)
+    out["projection_basis"] = ("per_core_images_per_s x affinity_physical_cores (one process per physical core; "
+                               "assumes the per-core rate measured at `cores` processes holds)")
     return out
 
 
@@ -331,6 +417,24 @@ def single_image(cx, h=3000, w=4000, iters=20):
     del t
     torch.cuda.empty_cache()
     return {"workload": f"1 x {h}x{w} RGB8 per call, full report, median of {iters}", **res}
+
+
+def config1(cx, iters=20):
+    """BASELINE config 1: one 1024x1024 uniform RGB8 image (splitmix64 seed
+    20241125) through the Python caller's get_report (core.py:171; the
+    reference's core.py:442-486), host buffer in -> Report out, median of
+    `iters`.  Parity is the tests' (tests/golden/uniform_1024.npz)."""
+    import numpy as np
+    from photohive_dsp_amd import core, synth
+    img = synth.uniform(1024, 1024, 20241125)
+    core.get_report(img)
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        core.get_report(img)
+        ts.append(time.perf_counter() - t0)
+    return {"workload": "1 x 1024x1024 uniform RGB8 (seed 20241125), get_report() from a host buffer, "
+                        f"median of {iters}", "gpu_get_report_ms": round(1000 * float(np.median(ts)), 3)}
 
 
 def legacy_entry(cx, h=3000, w=4000, iters=5):
@@ -612,8 +716,11 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before this process touches the GPU: the baseline's worker processes
         # start from a clean parent
-        procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
-        cpu = cpu_baseline(args.height, args.width, procs)
+        topo = cpu_topology()
+        procs = args.cpu_procs or topo["procs"]
+        if args.cpu_procs:
+            topo["procs_reason"] = f"--cpu-procs {args.cpu_procs}"
+        cpu = cpu_baseline(args.height, args.width, topo, procs)
     import torch
     ndev = torch.cuda.device_count()
     dev = local % ndev if ndev else local
@@ -653,6 +760,10 @@ def main(argv=None):
         extra["config4"] = config4(cx, args.config4_images)
         extra["config5"] = config5(cx, args.config5_images)
         if world == 1:
+            extra["config1"] = config1(cx)
+            if cpu is not None and "config1" in cpu:
+                extra["config1"]["cpu_ms_O2"] = cpu["config1"]["ms_O2"]
+                extra["config1"]["cpu_ms_O0"] = cpu["config1"]["ms_O0"]
             extra["config2_single"] = single_image(cx, args.height, args.width)
             extra["host_buffer"] = host_buffers(cx, args.height, args.width)
             extra["legacy_entry"] = legacy_entry(cx, args.height, args.width)
@@ -708,9 +819,21 @@ def main(argv=None):
                                 "sampling": "every launch of every 4th timed step, all ranks"}
             line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
         line.update(extra)
+        line["vs_baseline_note"] = ("null: BASELINE.md publishes no number for this metric (its only figures are "
+                                    "per-stage CPU seconds on an unstated image size, README.md:62-75)")
         if cpu is not None:
             line["cpu_baseline"] = cpu
-            line["vs_cpu_baseline"] = round(value / cpu["value"], 1)
+            # GPU / CPU ratios against the measured baseline and against the
+            # whole-affinity projection (both images/s, 4000x3000 full reports)
+            ratios = {"headline_device_resident": value}
+            if "host_buffer" in extra:
+                ratios["host_buffer"] = extra["host_buffer"]["images_per_s"]
+            if "legacy_entry" in extra:
+                ratios["legacy_entry"] = 1000.0 / extra["legacy_entry"]["ms"]
+            line["vs_cpu_baseline"] = {
+                k: {"images_per_s": round(v, 1), "x_measured": round(v / cpu["value"], 1),
+                    "x_projected_affinity": round(v / cpu["projected_affinity_images_per_s"], 1)}
+                for k, v in ratios.items()}
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -543,14 +543,15 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     const long npix = (long)height * width;
     const long nitems = (long)n * nchunks;
     const int ncell = HueCells::count(gp);
-    static bool attr = false;
-    if (!attr) {
+    // once per process, thread-safe (two lanes may launch concurrently)
+    static const bool attr = [] {
         (void)hipFuncSetAttribute((const void*)k_k1t<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_k1t<512, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
-        attr = true;
-    }
+        return true;
+    }();
+    (void)attr;
     // the two-block form runs a chunk in ~1.9x the time of the one-block form
     // (half a CU each): it wins when it has at least ~2 chunks per block
     // (measured at 16 x 732 chunks), not for a single image's 732 chunks

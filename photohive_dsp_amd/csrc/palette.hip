@@ -1516,12 +1516,11 @@ hipError_t launch_cutoffs_batch(const uint8_t* const* d_imgs, const uint8_t* con
     const size_t lds = K1Lds::area;
 #define PHD_KCUT_LAUNCH(A, T)                                                                               \
     do {                                                                                                    \
-        static bool attr = false;                                                                           \
-        if (!attr) {                                                                                        \
-            (void)hipFuncSetAttribute((const void*)k_cutoffs_b<A, T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                      160 * 1024);                                                          \
-            attr = true;                                                                                    \
-        }                                                                                                   \
+        /* a function-local static initialiser runs once, thread-safe */                                  \
+        static const bool attr_ = ((void)hipFuncSetAttribute((const void*)k_cutoffs_b<A, T>,                       \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), \
+                                   true);                                                                   \
+        (void)attr_;                                                                                        \
         phd_launch((k_cutoffs_b<A, T>), dim3(n_entries), dim3(kK1Threads), lds, st, d_imgs, npix,        \
                            nchunks, gp, fc, tabs, k255, entries, chunk_hist0, h_stride, rules0, b_stride);  \
     } while (0)
@@ -1558,12 +1557,10 @@ hipError_t launch_palette_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
 #define PHD_K3_LAUNCH(A, T)                                                                                 \
     do {                                                                                                    \
-        static bool attr = false;                                                                           \
-        if (!attr) {                                                                                        \
-            (void)hipFuncSetAttribute((const void*)k_palette_sums_b<A, T>,                                  \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);              \
-            attr = true;                                                                                    \
-        }                                                                                                   \
+        static const bool attr_ = ((void)hipFuncSetAttribute((const void*)k_palette_sums_b<A, T>,                  \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024), \
+                                   true);                                                                   \
+        (void)attr_;                                                                                        \
         phd_launch((k_palette_sums_b<A, T>), dim3(grid), dim3(kK3Threads), lds, st, d_imgs, npix,        \
                            nchunks, nitems, gp, fc, tabs, k255, rules0, off0, b_stride, nslots_img,         \
                            max_slots, out0, c_stride, k3_cshift(max_slots), env_ablate());                  \

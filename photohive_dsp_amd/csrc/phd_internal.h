@@ -92,6 +92,8 @@ struct PaletteDev {
     unsigned short* chunk_hist;   // [nchunks][TL]
     double* gsum = nullptr;       // fused K1: [3][TL] sum h, sum s, sum v per group
     unsigned* gcell = nullptr;    // fused K1: [HueCells::count] pixels per (group, hue cell)
+    unsigned long long* kd_sum = nullptr;   // statistics pass (stats.hip mode 3): [256] sum of
+                                            // max - min over the pixels of each max value
 };
 
 // Hue cells of the fused palette pass.  calculate_avg_hsv

@@ -1084,7 +1084,9 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
     const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
     const long npix = (long)height * width;
     const int nchunks = (int)((npix + kChunk - 1) / kChunk);
-    const size_t a_stride = al(6 * sizeof(unsigned long long)) + al(sizeof(double) * nchunks);
+    // A record: 6 moments | per-chunk s partials | 256 sums of d per max value
+    const size_t a_kd = al(6 * sizeof(unsigned long long)) + al(sizeof(double) * nchunks);
+    const size_t a_stride = a_kd + al(256 * sizeof(unsigned long long));
     const size_t rec = (size_t)n_images * a_stride, ptrs = al(sizeof(void*) * (size_t)n_images);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, rec + ptrs) || !ensure_pinned(c, rec + ptrs)) return -1;
     uint8_t* dw = (uint8_t*)c->d_ws;
@@ -1097,6 +1099,7 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
     PaletteDev pd{};
     pd.sums = (unsigned long long*)dw;
     pd.s_part = (double*)(dw + al(6 * sizeof(unsigned long long)));
+    pd.kd_sum = (unsigned long long*)(dw + a_kd);
     auto fail = [&](hipError_t e, const char* what) {
         set_error(std::string("phd_hsv_stats_batch_device: ") + what + ": " + hipGetErrorString(e));
         return -1;
@@ -1118,8 +1121,14 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
         const uint8_t* a = hp + (size_t)i * a_stride;
         stats[i] = stats_from_sums((const unsigned long long*)a, npix);
         const double* sp = (const double*)(a + al(6 * sizeof(unsigned long long)));
+        // sum(s) = per-run s partials (the fp32 modes; in the exact mode only the
+        // partial final group and -(1 - 0.999999) per min == 0 < max pixel) +
+        // sum_m (sum of d at max m) / m (the exact mode; zero otherwise)
+        const unsigned long long* kd = (const unsigned long long*)(a + a_kd);
         double sacc = 0.0;
         for (int k = 0; k < nchunks; k++) sacc += sp[k];
+        for (int m = 1; m < 256; m++)
+            if (kd[m]) sacc += (double)kd[m] / (double)m;
         avg_saturation[i] = sacc / (double)npix;
     }
     return 0;

@@ -45,31 +45,66 @@ HostPool* copy_pool() {
     return p;
 }
 
+static bool staged_upload() {
+    static const bool staged = getenv("PHD_UPLOAD") && !strcmp(getenv("PHD_UPLOAD"), "staged");
+    return staged;
+}
+
+// The streams and events every upload path uses.  c->h2d is set last, so a
+// failed setup leaves the context without it and the next call retries; each
+// failure names itself.
 bool upload_init(Context* c) {
     if (c->h2d) return true;
-    if (hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->h2d2, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_h2d2, device_event_flags()) != hipSuccess ||
-        hipHostMalloc((void**)&c->h2d_slots, kSlotBytes * kSlots, hipHostMallocDefault) != hipSuccess) {
-        set_error("upload staging setup failed");
+    hipStream_t h2d = nullptr;
+    if (!c->h2d2 && hipStreamCreateWithFlags(&c->h2d2, hipStreamNonBlocking) != hipSuccess) {
+        c->h2d2 = nullptr;
+        set_error("upload setup: second upload stream creation failed");
         return false;
     }
-    c->ev_slot.resize(kSlots);
-    for (auto& e : c->ev_slot)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
-    c->slot_used.assign(kSlots, 0);
+    if (!c->ev_h2d2 && hipEventCreateWithFlags(&c->ev_h2d2, device_event_flags()) != hipSuccess) {
+        c->ev_h2d2 = nullptr;
+        set_error("upload setup: upload event creation failed");
+        return false;
+    }
     for (auto& e : c->ev_up)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            e = nullptr;
+            set_error("upload setup: upload event creation failed");
+            return false;
+        }
+    if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess) {
+        set_error("upload setup: upload stream creation failed");
+        return false;
+    }
+    c->h2d = h2d;
+    return true;
+}
+
+// The pinned slot ring of the staged path (PHD_UPLOAD=staged only: the default
+// pageable path never touches it, so it is not allocated there).
+static bool staged_init(Context* c, std::string* why) {
+    if (c->h2d_slots) return true;
+    if (c->ev_slot.size() != (size_t)kSlots) c->ev_slot.assign(kSlots, nullptr);
+    for (auto& e : c->ev_slot)
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            e = nullptr;
+            *why = "upload setup: slot event creation failed";
+            return false;
+        }
+    uint8_t* slots = nullptr;
+    if (hipHostMalloc((void**)&slots, kSlotBytes * kSlots, hipHostMallocDefault) != hipSuccess) {
+        *why = "upload setup: pinned slot ring allocation failed";
+        return false;
+    }
+    c->slot_used.assign(kSlots, 0);
+    c->next_slot = 0;
+    c->h2d_slots = slots;
     return true;
 }
 
 // Enqueue the transfer of `bytes` contiguous host bytes to d_dst on c->h2d.
 // Returns once every chunk has been copied into a pinned slot (the caller's
 // buffer is no longer read); the DMA may still be running.
-static bool staged_upload() {
-    static const bool staged = getenv("PHD_UPLOAD") && !strcmp(getenv("PHD_UPLOAD"), "staged");
-    return staged;
-}
 
 int upload_streams() {
     static const int n = getenv("PHD_UPLOAD_STREAMS") ? std::min(2, std::max(1, atoi(getenv("PHD_UPLOAD_STREAMS"))))
@@ -84,6 +119,7 @@ bool upload_async(Context* c, uint8_t* d_dst, const uint8_t* src, size_t bytes, 
         if (e != hipSuccess) *why = std::string("upload failed: ") + hipGetErrorString(e);
         return e == hipSuccess && hipStreamSynchronize(us) == hipSuccess;
     }
+    if (!staged_init(c, why)) return false;
     HostPool* pool = copy_pool();
     for (size_t off = 0; off < bytes; off += kSlotBytes) {
         const int s = c->next_slot;

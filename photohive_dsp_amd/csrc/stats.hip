@@ -19,14 +19,25 @@
 //     one fp32 reciprocal per pair, summed in fp32 per item and in fp64 per run.
 //     M is raised to 1 for black pixels (d = 0).
 // rgb2hsv's s is d / max except 0.999999 for d == max (min == 0 < max,
-// src/image_processing.c:408-414).  By default those pixels add d / max = 1,
-// so S-bar is high by at most 1e-6 relative (fp32 rounding adds ~1e-7): inside
-// north_star's 1e-4 for the float fields.  The exact forms were measured and
-// cost the pass its HBM roofline -- at 3 bytes per pixel it sits at the
-// crossover where a few more VALU per pixel make it VALU-bound:
+// src/image_processing.c:408-414).
+//
+// Default, PHD_STATS_MODE=3 (the reference's width): s is never divided per
+// pixel.  sum(s) = sum_m (sum of d over the pixels with max = m) / m
+//                  - (1 - 0.999999) * #(min == 0 < max)
+// (a d == max pixel adds m / m = 1 to the first term; 1 - 0.999999 is exact in
+// fp64), so the pass only needs, per image, the exact integer sum of d per max
+// value m: ONE u32 LDS atomic per pixel into a per-lane copy of a 256-bucket
+// histogram (32 copies, padded to 257 so lanes fall on distinct banks), folded
+// into the image's u64 buckets when a run ends; the host finishes the sum in
+// fp64 (phd_hsv_stats_batch_device).  Within ~1e-15 of the reference's
+// sequential fp64 sum of the per-pixel doubles.
+//
+// The earlier fp32 forms (kept for measurement):
+//   PHD_STATS_MODE=0: fp32 pair sums, d == max pixels add 1: S-bar high by
+//                     <= 1e-6 relative; 0.71-0.74 of the HBM peak (round 2);
 //   PHD_STATS_MODE=1: + a count of min == 0 < max pixels (packed u16), each
 //                     taking (1 - 0.999999) off at the flush: ~1e-7 relative,
-//                     0.60-0.63 of the HBM peak against 0.71-0.74;
+//                     0.60-0.63;
 //   PHD_STATS_MODE=2: + compensated fp32 quotients and Kahan sums: ~2e-9, 0.57;
 //   (an fp64 v_rcp_f64 + Newton form: 0.54, not kept).
 // The full report's K1 (k1.hip) keeps the exact fp64 s.
@@ -61,10 +72,11 @@ struct StatAcc {
 };
 
 // 4 pixels (3 little-endian words w0..w2 = r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3).
-// kMode 0: plain fp32 pair sums (round 1); 1: + the 0.999999 rule (default);
-// 2: + compensated quotients and Kahan sums
+// kMode 0: plain fp32 pair sums (round 1); 1: + the 0.999999 rule; 2: +
+// compensated quotients and Kahan sums; 3 (default): d added to bucket max of
+// this lane's LDS histogram copy `hk` + the 0.999999 count
 template <int kMode>
-__device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, StatAcc& a) {
+__device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, StatAcc& a, unsigned* hk) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as_u16x2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
     const u16x2 r13 = as_u16x2(__builtin_amdgcn_perm(w2, w0, 0x0c050c03u));
@@ -89,6 +101,16 @@ __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, Sta
     const u16x2 n02 = __builtin_elementwise_min(__builtin_elementwise_min(r02, g02), b02);
     const u16x2 n13 = __builtin_elementwise_min(__builtin_elementwise_min(r13, g13), b13);
     const u16x2 d02 = m02 - n02, d13 = m13 - n13;
+    if constexpr (kMode == 3) {
+        atomicAdd(&hk[m02.x], (unsigned)d02.x);
+        atomicAdd(&hk[m13.x], (unsigned)d13.x);
+        atomicAdd(&hk[m02.y], (unsigned)d02.y);
+        atomicAdd(&hk[m13.y], (unsigned)d13.y);
+        const u16x2 zero = {0, 0};
+        a.n1 += (u16x2)((n02 == zero) & (m02 != zero)) & one;
+        a.n1 += (u16x2)((n13 == zero) & (m13 != zero)) & one;
+        return;
+    }
     const u16x2 M02 = __builtin_elementwise_max(m02, one), M13 = __builtin_elementwise_max(m13, one);
     const u16x2 S02 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M02), as_u32(M02), 16));
     const u16x2 S13 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M13), as_u32(M13), 16));
@@ -128,12 +150,21 @@ __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, Sta
 // (or every 1024 items, so the u32 squares cannot overflow: 1024 * 8 groups *
 // 4 * 255^2 < 2^32).  Outputs as K1's statistics-only form: out.sums (6 u64,
 // atomics) and out.s_part[first chunk of the run] (one fp64 per run).
+constexpr int kHistCopies = 32, kHistPad = 257;
+
 template <bool kNT, int kMode>
 __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* const* __restrict__ imgs, long npix,
                                                               int nchunks, long nitems, PaletteDev out,
                                                               long a_stride) {
     __shared__ unsigned long long red[kStThreads / 64][8];
+    // kMode 3: sum of d per max value, one copy per lane of a half-wave
+    __shared__ unsigned hist[kMode == 3 ? kHistCopies * kHistPad : 1];
     const int tid = threadIdx.x;
+    unsigned* hk = hist + (kMode == 3 ? (tid & (kHistCopies - 1)) * kHistPad : 0);
+    if constexpr (kMode == 3) {
+        for (int i = tid; i < kHistCopies * kHistPad; i += kStThreads) hist[i] = 0u;
+        __syncthreads();
+    }
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
     const long full_end = npix & ~3L;                       // groups wholly inside the image
@@ -164,14 +195,14 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
                 }
             }
 #pragma unroll
-            for (int st = 0; st < kStGroups; st++) stat4<kMode>(w[st][0], w[st][1], w[st][2], a);
+            for (int st = 0; st < kStGroups; st++) stat4<kMode>(w[st][0], w[st][1], w[st][2], a, hk);
         } else {
 #pragma unroll 1
             for (int st = 0; st < kStGroups; st++) {
                 const long p0 = base + 4L * tid + 4L * kStThreads * st;
                 if (p0 < full_end) {
                     gu32s* q = (gu32s*)(ip + 3 * p0);
-                    stat4<kMode>(q[0], q[1], q[2], a);
+                    stat4<kMode>(q[0], q[1], q[2], a, hk);
                 }
             }
         }
@@ -217,6 +248,20 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
                 reinterpret_cast<double*>(red[wv])[6] = sw;
             }
             __syncthreads();
+            if constexpr (kMode == 3) {
+                // the run's buckets into the image's (exact u64 sums, any order)
+                if (tid < 256) {
+                    unsigned long long b = 0;
+#pragma unroll 8
+                    for (int k = 0; k < kHistCopies; k++) {
+                        b += hist[k * kHistPad + tid];
+                        hist[k * kHistPad + tid] = 0u;
+                    }
+                    if (b)
+                        atomicAdd(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(out.kd_sum) +
+                                                                        cimg * a_stride) + tid, b);
+                }
+            }
             if (tid < 6) {
                 unsigned long long t = 0;
                 for (int q = 0; q < kStThreads / 64; q++) t += red[q][tid];
@@ -248,18 +293,25 @@ hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     // against 0.70-0.72 with plain loads (PHD_STATS_PLAIN=1)
     static const bool nt = getenv("PHD_STATS_PLAIN") == nullptr;
     // PHD_STATS_MODE (config 3, 512 x 1080p, fraction of the 8 TB/s peak):
-    // 0 (default) fp32 pair sums 0.71-0.74; 1 + the 0.999999 count 0.60-0.63;
-    // 2 + compensated quotients 0.57; an fp64 rcp + Newton form measured 0.54
-    static const int mode = getenv("PHD_STATS_MODE") ? atoi(getenv("PHD_STATS_MODE")) : 0;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_rgb_stats<true, 1>, kStThreads, 0) !=
-            hipSuccess || per_cu < 1)
-        per_cu = 1;
-    const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
+    // 3 (default) exact sum of d per max value; 0 fp32 pair sums 0.71-0.74 (round
+    // 2); 1 + the 0.999999 count 0.60-0.63; 2 + compensated quotients 0.57
+    static const int mode = getenv("PHD_STATS_MODE") ? atoi(getenv("PHD_STATS_MODE")) : 3;
 #define PHD_ST(NT, M)                                                                                          \
-    phd_launch((k_rgb_stats<NT, M>), dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0, \
-               a_stride)
-    if (mode == 0) {
+    do {                                                                                                       \
+        /* the persistent grid is sized for the variant launched */                                            \
+        static const int per_cu_ = [] {                                                                        \
+            int b = 0;                                                                                         \
+            return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, (const void*)k_rgb_stats<NT, M>,           \
+                                                                kStThreads, 0) == hipSuccess && b > 0 ? b : 1; \
+        }();                                                                                                   \
+        const int grid = (int)std::min<long>(nitems, (long)per_cu_ * num_cus());                               \
+        phd_launch((k_rgb_stats<NT, M>), dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems,   \
+                   out0, a_stride);                                                                            \
+    } while (0)
+    if (mode == 3 && out0.kd_sum) {
+        if (nt) PHD_ST(true, 3);
+        else PHD_ST(false, 3);
+    } else if (mode == 0) {
         if (nt) PHD_ST(true, 0);
         else PHD_ST(false, 0);
     } else if (mode == 2) {
