@@ -35,10 +35,9 @@
 //
 // log(p) for the bins: a run's sum of log p is the log of its product.  The
 // frexp mantissas (in [1/2, 1)) multiply in fp64 and the exponents add, and
-// one fp32 log of the mantissa product closes the run: e ln2 + log(m).  The
-// absolute error is <= 2e-7 per run (~10 elements), against bin averages of
-// order 10 (north_star tolerance: 1e-4 relative).  The max and the p >= 1 test
-// stay in fp64.
+// one fp64 log of the mantissa product closes the run: e ln2 + log(m), as
+// pgm_normalize_fft's per-element fp64 log (src/fft_processing.c:196-199) to
+// ~1e-15 per run.  The max and the p >= 1 test stay in fp64.
 #include <cstdlib>
 
 // Nothing in this file needs the reference's rounding (the FFT only has to be
@@ -68,6 +67,56 @@ typedef unsigned u32x3a __attribute__((ext_vector_type(3), aligned(4)));
 __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
     const unsigned x = (b >> 2) == 0 ? w.x : ((b >> 2) == 1 ? w.y : w.z);   // b is a constant
     return (x >> (8 * (b & 3))) & 255;
+}
+
+// One thread's walk over E consecutive rows of a column: p per row in LDS
+// (lgb[r0 + j]), bin ids packed two per word (bmw).  Contiguous rows of one
+// bin form a run whose sum of log p is the log of its product: the frexp
+// mantissas multiply (>= 2^-E, no underflow), the exponents add, and one fp64
+// log closes the run (pgm_normalize_fft's fp64 log, src/fft_processing.c:
+// 196-199).  Each run adds bin_scale fixed point to its bin with one LDS
+// atomic (order-independent sums).  A thread's first two runs are kept in
+// registers and logged after the walk: a wave then evaluates the fp64 log at
+// most twice (plus the rare third run of a thread), where logging inside the
+// unrolled walk ran it on almost every row (some lane of 64 changes bin there).
+template <int E>
+__device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0, int rend, const unsigned* bmw,
+                                          unsigned long long* bsum, double bscale) {
+    auto flush = [&](int b, double m, int e) {
+        const double acc = fmax((double)e * 0.69314718055994530942 + log(m), 0.0);
+        atomicAdd(&bsum[b], bin_fixed(acc, bscale));
+    };
+    int cur = -1, esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
+    double mprod = 1.0, m0 = 1.0, m1 = 1.0;
+    auto close = [&]() {
+        if (n == 0) {
+            b0 = cur; m0 = mprod; e0 = esum; n = 1;
+        } else if (n == 1) {
+            b1 = cur; m1 = mprod; e1 = esum; n = 2;
+        } else {
+            flush(cur, mprod, esum);
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < E; j++) {
+        const int r = r0 + j;
+        if (r < rend) {
+            const double pv = lgb[r];
+            const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
+            if (bin != cur) {
+                if (cur >= 0) close();
+                cur = bin;
+                mprod = 1.0;
+                esum = 0;
+            }
+            int e;
+            mprod *= frexp(pv, &e);
+            esum += e;
+        }
+    }
+    if (cur >= 0) close();
+    if (n > 0) flush(b0, m0, e0);
+    if (n > 1) flush(b1, m1, e1);
 }
 
 template <int W, int T, int... Rs>
@@ -420,36 +469,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         if (K::P0R && u + 1 < c1 && !(ablate & 4)) fetch0(pair_at(u + 1));
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
-        // few tens of rows along a column), in bin_scale fixed point so that the
-        // sums do not depend on the order of the atomics.  A run's sum of log p
-        // is log of the product: the frexp mantissas multiply (>= 2^-E, no
-        // underflow), the exponents add, one fp32 log of the mantissa product per run.
-        if (!(ablate & 2)) {
-            int cur = -1, esum = 0;
-            double mprod = 1.0;
-            auto flush = [&]() {
-                const double acc = fmax((double)esum * 0.69314718055994530942 + (double)__logf((float)mprod), 0.0);
-                atomicAdd(&bsum[cur], bin_fixed(acc, bscale));
-            };
-#pragma unroll
-            for (int j = 0; j < K::E; j++) {
-                const int u = ht * K::E + j;
-                if ((H % K::E == 0 && K::E * T == H) || u < H) {
-                    const double pv = lgb[u];
-                    const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
-                    if (bin != cur) {
-                        if (cur >= 0) flush();
-                        cur = bin;
-                        mprod = 1.0;
-                        esum = 0;
-                    }
-                    int e;
-                    mprod *= frexp(pv, &e);
-                    esum += e;
-                }
-            }
-            if (cur >= 0) flush();
-        }
+        // few tens of rows along a column; walk_runs)
+        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, bmw, bsum, bscale);
         __syncthreads();
     }
 #undef PHD_COL_FETCH
@@ -464,6 +485,200 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         fmax_part[blockIdx.x] = m;
     }
     for (int i = tid; i < nbins && !K::GB && !(ablate & 8); i += NT) {
+        const unsigned long long t = lb[i];
+        if (t != 0ull) atomicAdd(&bin_sums[i], t);
+    }
+}
+
+// ---- column pass, LDS-DMA form (CPB flag 64) ---------------------------------
+//
+// One block of 2T threads per CU, two columns at a time (thread group g = tid / T
+// takes column 2 kp + g of the 64-byte tile kp, the partner block b ^ 8 on the
+// same XCD the other tile of the 128-byte line), the next two columns STREAMED
+// INTO LDS WHILE THE CURRENT ONES FINISH: as soon as every thread holds its
+// last-pass inputs in registers the column buffers are free, and each wave
+// issues global_load_lds_dwordx4 (64 rows x 16 B of its group's next column per
+// instruction, written lane-linear into the buffer: no VGPRs, no ds_write).
+// The last pass, p = re^2 + im^2, the max and the run binning of the current
+// columns then run while the loads are in flight; the loop head waits for them
+// (vmcnt) and a barrier publishes them.  The k_cols_ct form instead issues a
+// column's loads at the start of its step and waits for them at once (the
+// latency is hidden only by the other resident block).
+//
+// LDS: two column buffers (2 x 16 H), p per row for one half of the rows of
+// each column (2 x 8 ceil(H/2): the walk runs over the two halves in turn),
+// the twiddles and the image's polar bins (one copy per CU; 8 nbins).  At H =
+// 3000 and 72 x 40 bins: 145.7 KB.
+template <int H, int T, int CPB, int... Rs>
+struct GlK {
+    using PL = Plan<H, T, 1, Rs...>;
+    using L = typename PL::Last;
+    static constexpr int R = H / L::NB;                       // last radix
+    static constexpr int NTW = tw_entries<1, Rs...>();
+    static constexpr int P = (H + 1) / 2;                     // row pairs
+    static constexpr int HH = (H + 1) / 2;                    // rows per walk half
+    static constexpr int E = (HH + T - 1) / T;                // walk rows per thread per half
+    static constexpr int NG = (H + 63) / 64;                  // LDS-DMA instructions per column
+    static constexpr int NGW = (NG + T / 64 - 1) / (T / 64);  // ... per wave
+    static constexpr size_t off_lgb = sizeof(double2) * 2 * H;
+    static constexpr size_t off_tw = off_lgb + sizeof(double) * 2 * HH;
+    static constexpr size_t off_bins = off_tw + sizeof(double2) * NTW;
+    static size_t lds(int nbins) { return off_bins + sizeof(unsigned long long) * nbins; }
+    static_assert(T % 64 == 0 && HH % 2 == 0, "whole waves; even halves (dword bin-id loads)");
+    static_assert(Radices<Rs...>::product == H, "plan");
+};
+
+// one wave's 64 x 16 B: lane l's source `src` lands at LDS byte address
+// lds_dst + 16 l (M0 is written and restored in the same statement)
+__device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int H, int T, int CPB, int... Rs>
+__global__ __launch_bounds__(2 * T, 2 * T / 256) void k_cols_glds(
+    const double2* __restrict__ inter, int wf, const uint16_t* __restrict__ binmap, int nbins,
+    unsigned long long* __restrict__ bin_sums, double* __restrict__ fmax_part, const double2* __restrict__ twg,
+    const unsigned long long* __restrict__ sums, int width, double* __restrict__ dbg, double bscale) {
+    using K = GlK<H, T, CPB, Rs...>;
+    using L = typename K::L;
+    constexpr int R = K::R, E = K::E, HH = K::HH;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    double2* bufs = reinterpret_cast<double2*>(smem);
+    double* lgbs = reinterpret_cast<double*>(smem + K::off_lgb);
+    double2* tw = reinterpret_cast<double2*>(smem + K::off_tw);
+    unsigned long long* lb = reinterpret_cast<unsigned long long*>(smem + K::off_bins);
+    const int tid = threadIdx.x;
+    const int g = tid / T, ht = tid - g * T;                  // column of the tile, thread in the group
+    double2* buf = bufs + g * H;
+    double* lgb = lgbs + g * HH;
+    for (int i = tid; i < K::NTW; i += 2 * T) tw[i] = twg[i];
+    for (int i = tid; i < nbins; i += 2 * T) lb[i] = 0ull;
+    const int kpn = (wf + 1) / 2;                             // tiles (column pairs) per row pair
+    const int nunit = (kpn + 1) / 2;                          // 128-byte lines per row pair
+    const int tile = (int)((blockIdx.x >> 3) & 1);            // blocks b, b ^ 8: the two tiles of a line
+    const int nlog = (int)gridDim.x / 2;
+    const int lblk = (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
+    const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
+    auto pair_at = [&](int u) { return min(2 * u + tile, kpn - 1); };
+    // the group's column of tile kp into its buffer: wave w of the group issues
+    // instructions w, w + 4, ... (rows 64 i + lane), rows past H masked off
+    // (wave-uniform: a group is whole waves; readfirstlane puts it in an SGPR for M0)
+    const unsigned lds_buf = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(buf));
+    const int wv = ht >> 6, ln = ht & 63;
+    auto stream_in = [&](int kp) {
+        // row y = 64 i + lane; one instruction step (T rows) moves T / 2 row pairs
+        const double2* src = inter + ((size_t)kp * 2 + g) * 2 + (size_t)((64 * wv + ln) >> 1) * kpn * 4 + (ln & 1);
+        const size_t step = (size_t)(T / 2) * kpn * 4;
+#pragma unroll
+        for (int j = 0; j < K::NGW; j++) {
+            const int i = wv + j * (T / 64);
+            if (i < K::NG && 64 * i + ln < H)
+                glds16(src, __builtin_amdgcn_readfirstlane(lds_buf + (unsigned)(64 * i) * 16u));
+            src += step;
+        }
+    };
+    if (c0 < c1) stream_in(pair_at(c0));
+    double mx = 0.0;
+    for (int u = c0; u < c1; u++) {
+        const int kp = pair_at(u);
+        const int col = 2 * (2 * u + tile) + g;               // unclamped: past the last tile idles
+        const bool live = col < wf;
+        // this thread's bin ids: rows ht E .. ht E + E - 1 of each half (64 B of
+        // padding after the table covers the last thread's over-read)
+        unsigned bmw[2][E / 2];
+        {
+            const uint16_t* bcol = binmap + (size_t)(live ? col : 0) * H + ht * E;
+            const bool any = ht * E < HH;                     // threads past the half's end walk nothing
+#pragma unroll
+            for (int h2 = 0; h2 < 2; h2++)
+#pragma unroll
+                for (int j = 0; j < E / 2; j++)
+                    bmw[h2][j] = any ? reinterpret_cast<const unsigned*>(bcol + h2 * HH)[j] : 0u;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the streamed columns have landed
+        __syncthreads();
+        if (kp == 0) {                                        // block-uniform
+            // remove_dc_bias (src/blur_profile.c:233-238) on column 0 (see k_cols_ct)
+            if (col == 0) {
+                const double n = (double)H * (double)width;
+                const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
+                                    (double)sums[2] / 255.0 / n) / 3.0;
+                const double dc = (double)width * avg;
+                for (int y = ht; y < H; y += T) buf[y].x -= dc;
+            }
+            __syncthreads();
+        }
+        K::PL::all_but_last(buf, tw, ht);
+        double2 v[L::ROUNDS][R];
+        L::load(buf, v, ht);
+        // the bin ids are consumed here, before the next columns' loads are issued
+        // (a plain load's first use waits for every vector-memory operation)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; h2++)
+#pragma unroll
+            for (int j = 0; j < E / 2; j++) asm volatile("" ::"v"(bmw[h2][j]));
+        __syncthreads();                                      // every thread holds its inputs: buffers free
+        if (u + 1 < c1) stream_in(pair_at(u + 1));
+        L::compute(v, tw + K::PL::last_tw_offset, ht);
+        // p per output; rows of the first half go to LDS at once, the second
+        // half's stay in registers until the first half has been walked (row
+        // b + k NB is in the first half for k < KH when NB divides HH)
+        constexpr bool SPLITK = L::ROUNDS == 1 && HH % L::NB == 0;
+        constexpr int KH = SPLITK ? HH / L::NB : R;
+        double pw[L::ROUNDS][R];
+#pragma unroll
+        for (int q = 0; q < L::ROUNDS; q++) {
+            const int b = ht + q * T;
+            if (L::active(b)) {
+#pragma unroll
+                for (int k = 0; k < R; k++) {
+                    const double2 X = v[q][k];
+                    const double p = X.x * X.x + X.y * X.y;          // src/fft_processing.c:49
+                    if (live) mx = fmax(mx, p);
+                    if (dbg && live) dbg[(size_t)col * H + b + k * L::NB] = p;
+                    const double pc = (live && p >= 1) ? p : 1.0;   // src/fft_processing.c:197-198
+                    if (SPLITK && k < KH) lgb[b + k * L::NB] = pc;
+                    else pw[q][k] = pc;
+                }
+            }
+        }
+#pragma unroll
+        for (int h2 = 0; h2 < 2; h2++) {
+            if (!SPLITK || h2 == 1) {
+                // p of the half's rows to LDS (tested per element unless SPLITK)
+#pragma unroll
+                for (int q = 0; q < L::ROUNDS; q++) {
+                    const int b = ht + q * T;
+                    if (L::active(b)) {
+#pragma unroll
+                        for (int k = SPLITK ? KH : 0; k < R; k++) {
+                            const int y = b + k * L::NB;
+                            if (SPLITK || (y >= HH) == (h2 == 1)) lgb[y - h2 * HH] = pw[q][k];
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            // contiguous runs of one bin, one LDS atomic per run (walk_runs)
+            walk_runs<E>(lgb, ht * E, HH, bmw[h2], lb, bscale);
+            __syncthreads();
+        }
+    }
+    // block max -> one partial per block; non-zero bins -> the image's sums
+    mx = wave_max(mx);
+    double* red = lgbs;
+    if (lane_id() == 0) red[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        double m = 0.0;
+        for (int w = 0; w < (2 * T) / 64; w++) m = fmax(m, red[w]);
+        fmax_part[blockIdx.x] = m;
+    }
+    for (int i = tid; i < nbins; i += 2 * T) {
         const unsigned long long t = lb[i];
         if (t != 0ull) atomicAdd(&bin_sums[i], t);
     }
@@ -497,8 +712,20 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
     return hipGetLastError();
 }
 
+// column-pass LDS bytes of a plan (CPB flag 64: the LDS-DMA form)
+template <int H, int T, int CPB, int... Rs>
+size_t cols_lds(int nbins) {
+    if constexpr ((CPB & 64) != 0) return GlK<H, T, CPB, Rs...>::lds(nbins);
+    else return ColK<H, T, CPB, Rs...>::lds(nbins);
+}
+
 template <int H, int T, int CPB, int... Rs>
 int cols_grid(int, int nbins) {
+    if constexpr ((CPB & 64) != 0) {
+        int g = resident_grid(k_cols_glds<H, T, CPB, Rs...>, 2 * T, cols_lds<H, T, CPB, Rs...>(nbins));
+        g = g / 16 * 16;                                    // XCD pairs b, b ^ 8
+        return g < 16 ? 16 : g;
+    }
     int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
     if ((CPB & 3) == 2) {
         g = g / 16 * 16;                                    // XCD pairs b, b^8
@@ -512,10 +739,14 @@ template <int H, int T, int CPB, int... Rs>
 hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st) {
-    const size_t lds = ColK<H, T, CPB, Rs...>::lds(nbins);
-    phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3((CPB & 3) * T), lds,
-                       st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf),
-                       g_ablate);
+    const size_t lds = cols_lds<H, T, CPB, Rs...>(nbins);
+    if constexpr ((CPB & 64) != 0)
+        phd_launch((k_cols_glds<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3(2 * T), lds,
+                   st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf));
+    else
+        phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3((CPB & 3) * T),
+                   lds, st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf),
+                   g_ablate);
     return hipGetLastError();
 }
 
@@ -570,7 +801,7 @@ bool ct_cols_plan(int h, std::vector<int>* radices) {
 size_t fft_cols_ct_lds(int h, int nbins) {
     const int n_ = h;
 #define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) return ColK<N, T, __VA_ARGS__>::lds(nbins);
+    if (n_ == N && V == v_) return cols_lds<N, T, __VA_ARGS__>(nbins);
     PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return 0;

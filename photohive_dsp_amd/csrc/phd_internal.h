@@ -275,6 +275,7 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 9, 256, 33, 15, 10, 20)    \
     X(3000, 10, 256, 33, 15, 20, 10)   \
     X(3000, 11, 256, 33, 25, 12, 10)   \
+    X(3000, 12, 256, 66, 15, 10, 20)   \
     X(6000, 0, 512, 5, 15, 20, 20)     \
     X(6000, 1, 512, 5, 10, 20, 30)     \
     X(4000, 0, 320, 5, 10, 20, 20)     \

@@ -18,10 +18,11 @@ pytestmark = pytest.mark.gpu
 
 FLOAT_RTOL = 1e-4          # north_star tolerance for float fields
 TIGHT_RTOL = 1e-9          # what fp64 actually delivers; tracked, not the contract
-# the compile-time column pass takes log(p) as e ln2 + fp32 log(mantissa)
-# (<= 2e-7 absolute per element, fft_ct.hip): bins of 12 MP images land within
-# ~4e-9 of the reference; tracked, not the contract
-BINS_TIGHT_RTOL = 1e-8
+# the column passes sum log(p) in fp64 (fft_ct.hip: e ln2 + fp64 log of each
+# run's mantissa product) in bin_scale fixed point; what remains is the FFT
+# (ours vs pocketfft standing in for FFTW) and the fixed-point rounding:
+# tracked, not the contract
+BINS_TIGHT_RTOL = 1e-10
 
 CASES = golden_manifest()["cases"]
 
@@ -87,7 +88,7 @@ def test_report_matches_reference_fixture(case):
     # and the tighter bar fp64 actually reaches (reported separately for the record)
     st = rep.rgb_stats
     np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], g["stats"], rtol=TIGHT_RTOL)
-    np.testing.assert_allclose(np.array(rep.blur_profile.bins), g["bins"], rtol=BINS_TIGHT_RTOL, atol=1e-14)
+    np.testing.assert_allclose(np.array(rep.blur_profile.bins), g["bins"], rtol=BINS_TIGHT_RTOL, atol=1e-13)
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
@@ -187,11 +188,22 @@ def test_hsv_stats_batch_config3_shape():
     np.testing.assert_allclose(sat[0], orc.palette(img)["average_saturation"], rtol=STATS_SAT_RTOL)
 
 
-# The statistics-only pass (stats.hip) sums s in fp32 per pixel pair and lets
-# d == max pixels add 1 instead of rgb2hsv's 0.999999: S-bar within 2e-6
-# relative (north_star allows 1e-4 for float fields); the moments are exact.
-# PHD_STATS_MODE=1 / 2 (closer forms, slower; stats.hip) are within 3e-7 / 5e-9.
-STATS_SAT_RTOL = {0: 2e-6, 1: 3e-7, 2: 5e-9}[int(os.environ.get("PHD_STATS_MODE", "0"))]
+# The statistics-only pass (stats.hip).  Default (PHD_STATS_MODE=3): exact
+# integer sums of d per max value, finished on the host in fp64 -- the
+# reference's width, within 1e-12 of its sequential fp64 sum.  The fp32 forms
+# kept for measurement: 0 (d == max adds 1, fp32 pair sums) within 2e-6, 1 / 2
+# within 3e-7 / 5e-9 (north_star allows 1e-4 for float fields).  The moments are
+# exact in every mode.
+STATS_MODE = int(os.environ.get("PHD_STATS_MODE", "3"))
+STATS_SAT_RTOL = {0: 2e-6, 1: 3e-7, 2: 5e-9, 3: 1e-12}[STATS_MODE]
+
+
+def stats_sat_rtol(npix):
+    """The exact mode is bounded by the reference's own rounding: its S-bar is a
+    sequential fp64 sum of npix per-pixel doubles (src/image_processing.c:533-540),
+    whose error bound is npix * 2^-53 relative (reached on images where every
+    pixel adds the same 0.999999)."""
+    return max(STATS_SAT_RTOL, npix * 2.0 ** -53) if STATS_MODE == 3 else STATS_SAT_RTOL
 
 
 @pytest.mark.parametrize("kind,h,w", [("uniform", 401, 577), ("black", 400, 400), ("saturated", 360, 1200),
@@ -225,7 +237,7 @@ def test_hsv_stats_pass_edge_images(kind, h, w):
         s1, a1 = hsv_stats_device(torch.from_numpy(img[None]).cuda())
         for st, sv in ((stats[i], sat[i]), (s1[0], a1[0])):
             np.testing.assert_allclose([st.Br, st.Bg, st.Bb, st.Cr, st.Cg, st.Cb], ref_st, rtol=TIGHT_RTOL)
-            np.testing.assert_allclose(sv, ref_sat, rtol=STATS_SAT_RTOL, atol=1e-15)
+            np.testing.assert_allclose(sv, ref_sat, rtol=stats_sat_rtol(h * w), atol=1e-15)
 
 
 def test_hsv_stats_pass_batch_512_1080p_consistency():
@@ -246,7 +258,7 @@ def test_hsv_stats_pass_batch_512_1080p_consistency():
         s1, a1 = hsv_stats_device(v[i:i + 1])
         assert [getattr(stats[i], f) for f in ("Br", "Bg", "Bb", "Cr", "Cg", "Cb")] == \
             [getattr(s1[0], f) for f in ("Br", "Bg", "Bb", "Cr", "Cg", "Cb")]
-        np.testing.assert_allclose(sat[i], a1[0], rtol=1e-9)
+        np.testing.assert_allclose(sat[i], a1[0], rtol=1e-14 if STATS_MODE == 3 else 1e-9)
     img = synth.uniform(h, w, 511)
     np.testing.assert_allclose(sat[511], orc.palette(img)["average_saturation"], rtol=STATS_SAT_RTOL)
     del t, v
