@@ -89,10 +89,11 @@ typedef struct Full_Report_Data {                      /* src/utilities.h:30-37 
 /* ---- legacy entry points (reference signatures) ------------------------- */
 
 /* Replaces get_full_report_data, src/interface.h:16-23 / src/interface.c:20-94.
- * Input: planar doubles in [0,1] (as utils.py:30-46 produces).  Inputs that are
- * exactly k/255.0 take the u8 path; any other doubles are rejected with a
- * message (round 1).  Returns NULL on the reference's error cases
- * (src/utilities.c:64-87) and on GPU errors. */
+ * Input: planar doubles (as utils.py:30-46 produces).  Inputs that are all
+ * exactly k/255.0 take the RGB8 pipeline; any other finite doubles run the fp64
+ * planar kernels (planar.hip: the reference's own double arithmetic); non-finite
+ * values are rejected with a message.  Returns NULL on the reference's error
+ * cases (src/utilities.c:64-87) and on GPU errors. */
 Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundaries* salient_characters,
                                        int h_partitions, int s_partitions, int v_partitions,
                                        double black_thresh, double gray_thresh,
@@ -246,10 +247,13 @@ int phd_profile_kernels(unsigned mask);
 int phd_profile_read(int kernel, double* total_ms, long* launches);
 
 /* Lanes a device batch of >= 16 images on the library's stream is split over
- * (1 or 2; default 2, or PHD_LANES).  Each lane is an independent context with
+ * (1 or 2; default 1, or PHD_LANES).  Each lane is an independent context with
  * its own streams and workspaces; the second runs on a library thread, so the
- * two halves' kernels, host phases and launch gaps overlap.  Results do not
- * depend on it.  lanes < 1 only queries.  Returns the previous setting. */
+ * two halves' kernels, host phases and launch gaps overlap (+8-11 % images/s at
+ * 4000x3000, bench.py's two_lanes object).  Results do not depend on it.  With
+ * two lanes, phd_last_timings and PHD_VERBOSE's stage lines cover lane 0's half
+ * of a batch only (the stage timings are per calling thread).  lanes < 1 only
+ * queries.  Returns the previous setting. */
 int phd_set_lanes(int lanes);
 
 #ifdef __cplusplus

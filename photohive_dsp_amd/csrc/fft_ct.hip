@@ -119,6 +119,21 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
     if (n > 1) flush(b1, m1, e1);
 }
 
+// The block's LDS bins into the image's sums (one atomic per non-zero bin).
+// With windows (win != nullptr) an LDS id is local to the block's rectangle of
+// (angle, radius) bins: global = first + (i / width) * nr + i % width.
+__device__ __forceinline__ void flush_bins(const unsigned long long* lb, int nlb, const int* __restrict__ win, int nr,
+                                           unsigned long long* __restrict__ bin_sums, int tid, int nt) {
+    const int first = win ? win[2 * blockIdx.x] : 0, width = win ? win[2 * blockIdx.x + 1] : 1;
+    for (int i = tid; i < nlb; i += nt) {
+        const unsigned long long t = lb[i];
+        if (t != 0ull) {
+            const int a = win ? i / width : 0;
+            atomicAdd(&bin_sums[win ? first + a * nr + (i - a * width) : i], t);
+        }
+    }
+}
+
 template <int W, int T, int... Rs>
 struct RowK {
     static constexpr int NTW = tw_entries<1, Rs...>();
@@ -311,6 +326,7 @@ struct ColK {
 template <int H, int T, int CPB, int... Rs>
 __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter, int wf,
                                                      const uint16_t* __restrict__ binmap, int nbins,
+                                                     const int* __restrict__ win, int nr,
                                                      unsigned long long* __restrict__ bin_sums, double* __restrict__ fmax_part,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums, int width,
@@ -484,47 +500,42 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         for (int w = 0; w < (NT + 63) / 64; w++) m = fmax(m, red[w]);
         fmax_part[blockIdx.x] = m;
     }
-    for (int i = tid; i < nbins && !K::GB && !(ablate & 8); i += NT) {
-        const unsigned long long t = lb[i];
-        if (t != 0ull) atomicAdd(&bin_sums[i], t);
-    }
+    if (!K::GB && !(ablate & 8)) flush_bins(lb, nbins, win, nr, bin_sums, tid, NT);
 }
 
 // ---- column pass, LDS-DMA form (CPB flag 64) ---------------------------------
 //
-// One block of 2T threads per CU, two columns at a time (thread group g = tid / T
-// takes column 2 kp + g of the 64-byte tile kp, the partner block b ^ 8 on the
-// same XCD the other tile of the 128-byte line), the next two columns STREAMED
-// INTO LDS WHILE THE CURRENT ONES FINISH: as soon as every thread holds its
-// last-pass inputs in registers the column buffers are free, and each wave
-// issues global_load_lds_dwordx4 (64 rows x 16 B of its group's next column per
-// instruction, written lane-linear into the buffer: no VGPRs, no ds_write).
-// The last pass, p = re^2 + im^2, the max and the run binning of the current
-// columns then run while the loads are in flight; the loop head waits for them
-// (vmcnt) and a barrier publishes them.  The k_cols_ct form instead issues a
-// column's loads at the start of its step and waits for them at once (the
-// latency is hidden only by the other resident block).
+// The k_cols_ct schedule (one column per block of T threads, blocks b, b^8,
+// b^16, b^24 of an XCD taking the four columns of the same 128-byte lines, two
+// blocks per CU), with the NEXT COLUMN STREAMED INTO LDS WHILE THE CURRENT ONE
+// FINISHES: as soon as every thread holds its last-pass inputs in registers the
+// column buffer is free, and each wave issues global_load_lds_dwordx4 (64 rows
+// x 16 B per instruction, written lane-linear into the buffer: no VGPRs, no
+// ds_write).  The last pass, p = re^2 + im^2, the max and the run binning of the
+// current column then run while the loads are in flight; the loop head waits
+// for them (vmcnt) and a barrier publishes them.  k_cols_ct instead issues a
+// column's loads at the start of its step and waits for them at once.
 //
-// LDS: two column buffers (2 x 16 H), p per row for one half of the rows of
-// each column (2 x 8 ceil(H/2): the walk runs over the two halves in turn),
-// the twiddles and the image's polar bins (one copy per CU; 8 nbins).  At H =
-// 3000 and 72 x 40 bins: 145.7 KB.
+// LDS: the column (16 H), p per row for one half of the rows (8 ceil(H/2): the
+// walk runs over the two halves in turn, so the column buffer is free for the
+// next column's rows), the twiddles and the block's window of polar bins
+// (ColBins): at H = 3000 and 72 x 40 bins 48 + 12 + 2.6 + <= 14.2 KB, two blocks
+// per CU.
 template <int H, int T, int CPB, int... Rs>
 struct GlK {
     using PL = Plan<H, T, 1, Rs...>;
     using L = typename PL::Last;
     static constexpr int R = H / L::NB;                       // last radix
     static constexpr int NTW = tw_entries<1, Rs...>();
-    static constexpr int P = (H + 1) / 2;                     // row pairs
     static constexpr int HH = (H + 1) / 2;                    // rows per walk half
     static constexpr int E = (HH + T - 1) / T;                // walk rows per thread per half
     static constexpr int NG = (H + 63) / 64;                  // LDS-DMA instructions per column
     static constexpr int NGW = (NG + T / 64 - 1) / (T / 64);  // ... per wave
-    static constexpr size_t off_lgb = sizeof(double2) * 2 * H;
-    static constexpr size_t off_tw = off_lgb + sizeof(double) * 2 * HH;
+    static constexpr size_t off_lgb = sizeof(double2) * H;
+    static constexpr size_t off_tw = off_lgb + sizeof(double) * HH;
     static constexpr size_t off_bins = off_tw + sizeof(double2) * NTW;
-    static size_t lds(int nbins) { return off_bins + sizeof(unsigned long long) * nbins; }
-    static_assert(T % 64 == 0 && HH % 2 == 0, "whole waves; even halves (dword bin-id loads)");
+    static size_t lds(int nlb) { return off_bins + sizeof(unsigned long long) * nlb; }
+    static_assert(T % 64 == 0 && HH % 2 == 0 && E % 2 == 0, "whole waves; even halves (dword bin-id loads)");
     static_assert(Radices<Rs...>::product == H, "plan");
 };
 
@@ -539,40 +550,37 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
 }
 
 template <int H, int T, int CPB, int... Rs>
-__global__ __launch_bounds__(2 * T, 2 * T / 256) void k_cols_glds(
-    const double2* __restrict__ inter, int wf, const uint16_t* __restrict__ binmap, int nbins,
+__global__ __launch_bounds__(T, T / 128) void k_cols_glds(
+    const double2* __restrict__ inter, int wf, const uint16_t* __restrict__ binmap, int nlb,
+    const int* __restrict__ win, int nr,
     unsigned long long* __restrict__ bin_sums, double* __restrict__ fmax_part, const double2* __restrict__ twg,
     const unsigned long long* __restrict__ sums, int width, double* __restrict__ dbg, double bscale) {
     using K = GlK<H, T, CPB, Rs...>;
     using L = typename K::L;
     constexpr int R = K::R, E = K::E, HH = K::HH;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double2* bufs = reinterpret_cast<double2*>(smem);
-    double* lgbs = reinterpret_cast<double*>(smem + K::off_lgb);
+    double2* buf = reinterpret_cast<double2*>(smem);
+    double* lgb = reinterpret_cast<double*>(smem + K::off_lgb);
     double2* tw = reinterpret_cast<double2*>(smem + K::off_tw);
     unsigned long long* lb = reinterpret_cast<unsigned long long*>(smem + K::off_bins);
     const int tid = threadIdx.x;
-    const int g = tid / T, ht = tid - g * T;                  // column of the tile, thread in the group
-    double2* buf = bufs + g * H;
-    double* lgb = lgbs + g * HH;
-    for (int i = tid; i < K::NTW; i += 2 * T) tw[i] = twg[i];
-    for (int i = tid; i < nbins; i += 2 * T) lb[i] = 0ull;
-    const int kpn = (wf + 1) / 2;                             // tiles (column pairs) per row pair
-    const int nunit = (kpn + 1) / 2;                          // 128-byte lines per row pair
-    const int tile = (int)((blockIdx.x >> 3) & 1);            // blocks b, b ^ 8: the two tiles of a line
-    const int nlog = (int)gridDim.x / 2;
-    const int lblk = (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7));
+    for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
+    for (int i = tid; i < nlb; i += T) lb[i] = 0ull;
+    // k_cols_ct's schedule (cols_owners): quad q = (b >> 3) & 3 of an XCD takes
+    // column 2 (2 u + q / 2) + q % 2 of each of its 128-byte lines u
+    const int kpn = (wf + 1) / 2, nunit = (kpn + 1) / 2;
+    const int quad = (int)((blockIdx.x >> 3) & 3), half = quad & 1;
+    const int nlog = (int)gridDim.x / 4;
+    const int lblk = (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
     const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
-    auto pair_at = [&](int u) { return min(2 * u + tile, kpn - 1); };
-    // the group's column of tile kp into its buffer: wave w of the group issues
-    // instructions w, w + 4, ... (rows 64 i + lane), rows past H masked off
-    // (wave-uniform: a group is whole waves; readfirstlane puts it in an SGPR for M0)
+    auto pair_at = [&](int u) { return min(2 * u + (quad >> 1), kpn - 1); };
     const unsigned lds_buf = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(buf));
-    const int wv = ht >> 6, ln = ht & 63;
+    const int wv = tid >> 6, ln = tid & 63;
+    // the column (half `half` of tile kp) into the buffer: wave w issues
+    // instructions w, w + T/64, ... (rows 64 i + lane), rows past H masked off
     auto stream_in = [&](int kp) {
-        // row y = 64 i + lane; one instruction step (T rows) moves T / 2 row pairs
-        const double2* src = inter + ((size_t)kp * 2 + g) * 2 + (size_t)((64 * wv + ln) >> 1) * kpn * 4 + (ln & 1);
-        const size_t step = (size_t)(T / 2) * kpn * 4;
+        const double2* src = inter + ((size_t)kp * 2 + half) * 2 + (size_t)((64 * wv + ln) >> 1) * kpn * 4 + (ln & 1);
+        const size_t step = (size_t)(T / 2) * kpn * 4;       // T rows = T / 2 row pairs per instruction step
 #pragma unroll
         for (int j = 0; j < K::NGW; j++) {
             const int i = wv + j * (T / 64);
@@ -585,22 +593,22 @@ __global__ __launch_bounds__(2 * T, 2 * T / 256) void k_cols_glds(
     double mx = 0.0;
     for (int u = c0; u < c1; u++) {
         const int kp = pair_at(u);
-        const int col = 2 * (2 * u + tile) + g;               // unclamped: past the last tile idles
+        const int col = 2 * (2 * u + (quad >> 1)) + half;     // unclamped: past the last tile idles
         const bool live = col < wf;
-        // this thread's bin ids: rows ht E .. ht E + E - 1 of each half (64 B of
-        // padding after the table covers the last thread's over-read)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the streamed column has landed
+        __syncthreads();
+        // this thread's bin ids: rows tid E .. tid E + E - 1 of each half (issued
+        // after the wait above, so they are in flight during the passes)
         unsigned bmw[2][E / 2];
         {
-            const uint16_t* bcol = binmap + (size_t)(live ? col : 0) * H + ht * E;
-            const bool any = ht * E < HH;                     // threads past the half's end walk nothing
+            const uint16_t* bcol = binmap + (size_t)(live ? col : 0) * H + tid * E;
+            const bool any = tid * E < HH;                    // threads past the half's end walk nothing
 #pragma unroll
             for (int h2 = 0; h2 < 2; h2++)
 #pragma unroll
                 for (int j = 0; j < E / 2; j++)
                     bmw[h2][j] = any ? reinterpret_cast<const unsigned*>(bcol + h2 * HH)[j] : 0u;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the streamed columns have landed
-        __syncthreads();
         if (kp == 0) {                                        // block-uniform
             // remove_dc_bias (src/blur_profile.c:233-238) on column 0 (see k_cols_ct)
             if (col == 0) {
@@ -608,22 +616,22 @@ __global__ __launch_bounds__(2 * T, 2 * T / 256) void k_cols_glds(
                 const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
                                     (double)sums[2] / 255.0 / n) / 3.0;
                 const double dc = (double)width * avg;
-                for (int y = ht; y < H; y += T) buf[y].x -= dc;
+                for (int y = tid; y < H; y += T) buf[y].x -= dc;
             }
             __syncthreads();
         }
-        K::PL::all_but_last(buf, tw, ht);
+        K::PL::all_but_last(buf, tw, tid);
         double2 v[L::ROUNDS][R];
-        L::load(buf, v, ht);
-        // the bin ids are consumed here, before the next columns' loads are issued
+        L::load(buf, v, tid);
+        // the bin ids are consumed here, before the next column's loads are issued
         // (a plain load's first use waits for every vector-memory operation)
 #pragma unroll
         for (int h2 = 0; h2 < 2; h2++)
 #pragma unroll
             for (int j = 0; j < E / 2; j++) asm volatile("" ::"v"(bmw[h2][j]));
-        __syncthreads();                                      // every thread holds its inputs: buffers free
+        __syncthreads();                                      // every thread holds its inputs: buffer free
         if (u + 1 < c1) stream_in(pair_at(u + 1));
-        L::compute(v, tw + K::PL::last_tw_offset, ht);
+        L::compute(v, tw + K::PL::last_tw_offset, tid);
         // p per output; rows of the first half go to LDS at once, the second
         // half's stay in registers until the first half has been walked (row
         // b + k NB is in the first half for k < KH when NB divides HH)
@@ -632,7 +640,7 @@ __global__ __launch_bounds__(2 * T, 2 * T / 256) void k_cols_glds(
         double pw[L::ROUNDS][R];
 #pragma unroll
         for (int q = 0; q < L::ROUNDS; q++) {
-            const int b = ht + q * T;
+            const int b = tid + q * T;
             if (L::active(b)) {
 #pragma unroll
                 for (int k = 0; k < R; k++) {
@@ -652,7 +660,7 @@ __global__ __launch_bounds__(2 * T, 2 * T / 256) void k_cols_glds(
                 // p of the half's rows to LDS (tested per element unless SPLITK)
 #pragma unroll
                 for (int q = 0; q < L::ROUNDS; q++) {
-                    const int b = ht + q * T;
+                    const int b = tid + q * T;
                     if (L::active(b)) {
 #pragma unroll
                         for (int k = SPLITK ? KH : 0; k < R; k++) {
@@ -664,24 +672,21 @@ __global__ __launch_bounds__(2 * T, 2 * T / 256) void k_cols_glds(
             }
             __syncthreads();
             // contiguous runs of one bin, one LDS atomic per run (walk_runs)
-            walk_runs<E>(lgb, ht * E, HH, bmw[h2], lb, bscale);
+            walk_runs<E>(lgb, tid * E, HH, bmw[h2], lb, bscale);
             __syncthreads();
         }
     }
     // block max -> one partial per block; non-zero bins -> the image's sums
     mx = wave_max(mx);
-    double* red = lgbs;
+    double* red = lgb;
     if (lane_id() == 0) red[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
         double m = 0.0;
-        for (int w = 0; w < (2 * T) / 64; w++) m = fmax(m, red[w]);
+        for (int w = 0; w < T / 64; w++) m = fmax(m, red[w]);
         fmax_part[blockIdx.x] = m;
     }
-    for (int i = tid; i < nbins; i += 2 * T) {
-        const unsigned long long t = lb[i];
-        if (t != 0ull) atomicAdd(&bin_sums[i], t);
-    }
+    flush_bins(lb, nlb, win, nr, bin_sums, tid, T);
 }
 
 template <typename K>
@@ -722,9 +727,9 @@ size_t cols_lds(int nbins) {
 template <int H, int T, int CPB, int... Rs>
 int cols_grid(int, int nbins) {
     if constexpr ((CPB & 64) != 0) {
-        int g = resident_grid(k_cols_glds<H, T, CPB, Rs...>, 2 * T, cols_lds<H, T, CPB, Rs...>(nbins));
-        g = g / 16 * 16;                                    // XCD pairs b, b ^ 8
-        return g < 16 ? 16 : g;
+        int g = resident_grid(k_cols_glds<H, T, CPB, Rs...>, T, cols_lds<H, T, CPB, Rs...>(nbins));
+        g = g / 32 * 32;                                    // XCD quads b, b^8, b^16, b^24
+        return g < 32 ? 32 : g;
     }
     int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
     if ((CPB & 3) == 2) {
@@ -736,18 +741,45 @@ int cols_grid(int, int nbins) {
 }
 
 template <int H, int T, int CPB, int... Rs>
-hipError_t cols_ct(const double2* inter, int width, int wf, const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
+hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, unsigned long long* bin_sums,
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st) {
-    const size_t lds = cols_lds<H, T, CPB, Rs...>(nbins);
+    const size_t lds = cols_lds<H, T, CPB, Rs...>(cb.nlb);
+    const int grid = cb.grid > 0 ? cb.grid : cols_grid<H, T, CPB, Rs...>(wf, cb.nlb);
     if constexpr ((CPB & 64) != 0)
-        phd_launch((k_cols_glds<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3(2 * T), lds,
-                   st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf));
+        phd_launch((k_cols_glds<H, T, CPB, Rs...>), dim3(grid), dim3(T), lds, st, inter, wf, cb.map, cb.nlb, cb.win,
+                   cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf));
     else
-        phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(cols_grid<H, T, CPB, Rs...>(wf, nbins)), dim3((CPB & 3) * T),
-                   lds, st, inter, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf),
-                   g_ablate);
+        phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.map, cb.nlb,
+                   cb.win, cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate);
     return hipGetLastError();
+}
+
+// Which block processes each column (the kernels' schedules above): one
+// column per block, blocks b, b^8, b^16, b^24 taking the four columns of a
+// line; or a tile (two columns) per block, blocks b, b^8 the two tiles.
+template <int H, int T, int CPB, int... Rs>
+void cols_owners(int wf, int grid, std::vector<int>* owner) {
+    owner->assign(wf, -1);
+    const int kpn = (wf + 1) / 2, nunit = (kpn + 1) / 2;
+    const bool pairs = (CPB & 64) == 0 && (CPB & 3) == 2;
+    for (int b = 0; b < grid; b++) {
+        const int q = pairs ? (b >> 3) & 1 : (b >> 3) & 3;
+        const int nlog = pairs ? grid / 2 : grid / 4;
+        const int lblk = pairs ? (b >> 4) * 8 + (b & 7) : (b >> 5) * 8 + (b & 7);
+        const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
+        for (int u = c0; u < c1; u++) {
+            if (pairs) {
+                for (int g = 0; g < 2; g++) {
+                    const int col = 2 * (2 * u + q) + g;
+                    if (col < wf) (*owner)[col] = b;
+                }
+            } else {
+                const int col = 2 * (2 * u + (q >> 1)) + (q & 1);
+                if (col < wf) (*owner)[col] = b;
+            }
+        }
+    }
 }
 
 // the selected variant of length n, else variant 0
@@ -816,6 +848,18 @@ int fft_cols_ct_blocks(int height, int wf, int nbins) {
     return 0;
 }
 
+bool fft_cols_ct_owners(int height, int wf, int grid, std::vector<int>* owner) {
+    const int n_ = height;
+#define PHD_X(N, V, T, ...)                                  \
+    if (n_ == N && V == v_) {                                \
+        cols_owners<N, T, __VA_ARGS__>(wf, grid, owner);     \
+        return true;                                         \
+    }
+    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+#undef PHD_X
+    return false;
+}
+
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
                               const double* k255, const double2* tw, double2* inter, hipStream_t st,
                               unsigned long long* rsum) {
@@ -827,13 +871,13 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,
-                              int nbins, unsigned long long* bin_sums, double* fmax_part, const double2* tw,
+hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const ColBins& cb,
+                              unsigned long long* bin_sums, double* fmax_part, const double2* tw,
                               const unsigned long long* sums, double* dbg, hipStream_t st) {
     const int n_ = height;
 #define PHD_X(N, V, T, ...) \
     if (n_ == N && V == v_) \
-        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, binmap, nbins, bin_sums, fmax_part, tw, sums, dbg, st);
+        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, dbg, st);
     PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return hipErrorInvalidValue;

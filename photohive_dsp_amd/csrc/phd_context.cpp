@@ -153,7 +153,9 @@ int lanes_setting() {
     int l = g_lanes.load();
     if (l < 0) {
         const char* e = getenv("PHD_LANES");
-        l = e ? std::min(std::max(atoi(e), 1), kLanes) : kLanes;
+        // one lane unless asked for: the default is what bench.py's headline and
+        // roofline measure (each kernel launch alone on the GPU)
+        l = e ? std::min(std::max(atoi(e), 1), kLanes) : 1;
         g_lanes.store(l);
     }
     return l;
@@ -302,7 +304,44 @@ const double2* get_ct_twiddles(Context* c, int n, bool rows) {
     return d;
 }
 
-bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s) {
+// The compile-time column pass's bin windows for a table: the grid the
+// kernel's occupancy gives with the windows' LDS and the windows made for that
+// grid must agree (a window is sized by the columns a block owns, the grid by
+// the largest window), so iterate from the bins-free grid.  nullptr when no
+// window set is consistent, or when the windows would not put more blocks on
+// a CU than the full table does (measured: at the same occupancy the full
+// table is the faster, 55.7 against 60.0 us at 4000x3000; 4000-row columns at
+// two blocks per CU instead of one, 103.6 against 143.3 us).
+static const ColWin* get_col_windows(Context* c, const BlurTable& t, int width) {
+    static const int mode = getenv("PHD_COL_WINDOWS") ? atoi(getenv("PHD_COL_WINDOWS")) : 1;   // 0 off, 2 always
+    if (mode == 0) return nullptr;
+    const int nbins = t.na * t.nr;
+    const int g_full = fft_cols_ct_blocks(t.height, t.wf, nbins);
+    int grid = fft_cols_ct_blocks(t.height, t.wf, 1);
+    if (mode == 1 && grid <= g_full) return nullptr;
+    for (int it = 0; it < 3; it++) {
+        const auto key = std::make_tuple(t.height, width, t.nr, t.na, grid);
+        auto f = c->colwins.find(key);
+        const ColWin* w = nullptr;
+        if (f != c->colwins.end()) {
+            w = &f->second;
+        } else {
+            std::vector<int> owner;
+            ColWin cw;
+            if (!fft_cols_ct_owners(t.height, t.wf, grid, &owner) || !build_col_windows(t, grid, owner, &cw))
+                return nullptr;
+            w = &(c->colwins[key] = cw);
+        }
+        if (w->win_max >= nbins) return nullptr;
+        const int g2 = fft_cols_ct_blocks(t.height, t.wf, w->win_max);
+        if (g2 == grid) return (mode == 1 && grid <= g_full) ? nullptr : w;
+        grid = g2;
+    }
+    return nullptr;
+}
+
+bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
+                const BlurTable* tbl) {
     *s = FftSel{};
     static const bool force_generic = getenv("PHD_FFT_GENERIC") != nullptr;   // A/B experiments only
     bool ct = !force_generic && ct_rows_plan(width, nullptr) && ct_cols_plan(height, nullptr) &&
@@ -314,7 +353,14 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         s->tw_r = get_ct_twiddles(c, width, true);
         s->tw_c = get_ct_twiddles(c, height, false);
         if (!s->tw_r || !s->tw_c) return false;
-        s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
+        const ColWin* w = tbl ? get_col_windows(c, *tbl, width) : nullptr;
+        if (w) {
+            s->cbins = ColBins{w->d_lmap, w->d_win, w->win_max, tbl->nr, w->grid};
+            s->col_blocks = w->grid;
+        } else {
+            s->cbins = ColBins{tbl ? tbl->d_map : nullptr, nullptr, nbins, tbl ? tbl->nr : 0, 0};
+            s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
+        }
         return true;
     }
     if (!gfft_direct_ok(width) || !gfft_direct_ok(height)) return select_generic(c, height, width, nbins, s);
@@ -338,9 +384,10 @@ hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int 
 hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, int width, int wf,
                            const uint16_t* binmap, int nbins, unsigned long long* bin_sums, double* fmax_part,
                            const unsigned long long* sums, double* dbg, hipStream_t st) {
-    if (s.ct)
-        return launch_fft_cols_ct(inter, height, width, wf, binmap, nbins, bin_sums, fmax_part, s.tw_c, sums, dbg,
-                                  st);
+    if (s.ct) {
+        if (!s.cbins.map) return hipErrorInvalidValue;   // select_fft without a table
+        return launch_fft_cols_ct(inter, height, width, wf, s.cbins, bin_sums, fmax_part, s.tw_c, sums, dbg, st);
+    }
     if (dbg) return hipErrorNotSupported;
     if (s.generic) return generic_cols(s, const_cast<double2*>(inter), height, wf, binmap, nbins, bin_sums, fmax_part, st);
     return launch_fft_cols(inter, height, wf, s.pcol->plan, binmap, nbins, bin_sums, fmax_part, st);

@@ -67,12 +67,24 @@ bool decide_palette(const GridParams& gp, const GroupCenters& gc, const unsigned
 struct BlurTable {
     int height = 0, wf = 0, nr = 0, na = 0;
     std::vector<long long> counts;       // [na*nr]
+    std::vector<uint16_t> map;           // host [wf][height] (the column windows are made from it)
     uint16_t* d_map = nullptr;           // device [wf][height]
     int angle_bin_size = 0, radius_bin_size = 0;
+};
+// The compile-time column pass's per-block polar-bin windows for one table
+// and grid (ColBins, phd_internal.h): window-local bin ids, each block's first
+// bin and radius width, the largest window.
+struct ColWin {
+    int grid = 0, win_max = 0;
+    uint16_t* d_lmap = nullptr;          // device [wf][height]
+    int* d_win = nullptr;                // device [grid][2]
 };
 // Exact (phi_bin, r_bin) of every spectrum element, glibc atan2 + newton_int_sqrt
 // exactly as src/blur_profile.c:87-97 / 427-458.
 bool build_blur_table(int height, int width, int nr, int na, BlurTable* t);
+// The per-block windows of the column pass for `grid` blocks (owner[col] =
+// the block of each column): false when a window would not be smaller.
+bool build_col_windows(const BlurTable& t, int grid, const std::vector<int>& owner, ColWin* w);
 void vectorize_blur(const double* bins, int na, int nr, double streak, double mag, int denom,
                     Blur_Vector* out10);
 
@@ -151,6 +163,7 @@ struct Context {
     std::map<int, FftPlanHost> plans;
     std::map<std::pair<int, int>, double2*> ct_tw;  // (length, rows?) -> compile-time plan twiddles
     std::map<std::tuple<int, int, int, int>, BlurTable> tables;
+    std::map<std::tuple<int, int, int, int, int>, ColWin> colwins;   // (H, W, nr, na, grid)
     std::map<int, GfftPlan> gplans;                 // global-memory FFT plans by length
     double2* d_gbuf = nullptr;                      // generic 2-D path: row pairs + scratch
     size_t gbuf_bytes = 0;
@@ -245,7 +258,7 @@ private:
     std::thread th_;
 };
 LaneWorker* lane_worker();
-// lanes a large device batch is split over (PHD_LANES, default 2; phd_set_lanes)
+// lanes a large device batch is split over (PHD_LANES, default 1; phd_set_lanes)
 int lanes_setting();
 // The stream a call works on: the caller's, or (NULL) the library's own stream
 // ordered after every prior operation of the legacy null stream, so device
@@ -267,6 +280,7 @@ struct FftSel {
     const double2* tw_r = nullptr;
     const double2* tw_c = nullptr;
     int col_blocks = 0;   // entries of the per-block max partials
+    ColBins cbins;        // compile-time column pass: the bins it sums into (windows or the full table)
     // the generic path (a side above the LDS limit or with a large prime
     // factor): row pairs -> global row transforms -> split / transpose, then
     // the fused runtime column pass (cols_fused) or global column transforms
@@ -276,7 +290,10 @@ struct FftSel {
     const GfftPlan* gcol = nullptr;
     double2* gbuf = nullptr;
 };
-bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s);
+// tbl: the polar-bin table of the size (the compile-time column pass's bin
+// windows are made from it; nullptr: every block sums all na * nr bins)
+bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
+                const BlurTable* tbl);
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
                            const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st,
                            unsigned long long* rsum = nullptr);

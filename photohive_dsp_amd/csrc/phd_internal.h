@@ -262,6 +262,11 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 // of 4000 at 320 threads 126 us, 256 threads 130, (16 25 10) 164, 384
 // threads 182; rows of 6000 at 512 / 768 threads 93 us, 384 threads 103.
 // Columns of 3000 at 320 threads 73 us, 192 threads 67 (v0: 53-58).
+// Round 3: columns of 4000 at 256 threads 143 us with the full bin table (one
+// block per CU by LDS), 104 us with per-block bin windows (two blocks per CU,
+// ColBins), against 159-162 us at 320 threads: 256 threads is variant 0.
+// Variant 12 (flag 64): k_cols_glds, the next column streamed into LDS by
+// LDS-DMA during the current one's last pass and binning (needs the windows).
 #define PHD_CT_COLS(X)                 \
     X(3000, 0, 256, 5, 15, 10, 20)     \
     X(3000, 1, 384, 2, 5, 6, 10, 10)   \
@@ -275,19 +280,35 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 9, 256, 33, 15, 10, 20)    \
     X(3000, 10, 256, 33, 15, 20, 10)   \
     X(3000, 11, 256, 33, 25, 12, 10)   \
-    X(3000, 12, 256, 66, 15, 10, 20)   \
+    X(3000, 12, 256, 65, 15, 10, 20)   \
     X(6000, 0, 512, 5, 15, 20, 20)     \
     X(6000, 1, 512, 5, 10, 20, 30)     \
-    X(4000, 0, 320, 5, 10, 20, 20)     \
-    X(4000, 1, 256, 5, 10, 20, 20)     \
+    X(4000, 0, 256, 5, 10, 20, 20)     \
+    X(4000, 1, 320, 5, 10, 20, 20)     \
     X(2000, 0, 256, 5, 10, 10, 20)
 int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);
 bool ct_cols_plan(int h, std::vector<int>* radices);
-size_t fft_cols_ct_lds(int height, int nbins);
-// persistent grid of the column kernel (= entries of fmax_part)
-int fft_cols_ct_blocks(int height, int wf, int nbins);
+// The polar bins the compile-time column pass sums into.  Each block's
+// columns touch a rectangle of (angle, radius) bins, so a block can sum into an
+// LDS window of that rectangle (window-local ids in `map`, decoded through
+// `win` when the block adds its window to the image's bins) instead of all
+// na * nr bins: 1.1-14 KB instead of 23 KB of LDS at 72 x 40 bins, which lets
+// two column blocks share a CU where the full table did not fit beside them.
+struct ColBins {
+    const uint16_t* map = nullptr;   // [wf][height] bin ids: global (win == nullptr) or window-local
+    const int* win = nullptr;        // [grid][2] {global id of the window's first bin, window radius width}
+    int nlb = 0;                     // LDS bins: na * nr, or the largest window
+    int nr = 0;                      // radius_partitions (window decode)
+    int grid = 0;                    // the grid the windows were made for (0: from occupancy)
+};
+size_t fft_cols_ct_lds(int height, int nlb);
+// persistent grid of the column kernel (= entries of fmax_part) with nlb LDS bins
+int fft_cols_ct_blocks(int height, int wf, int nlb);
+// the block that processes each column (owner[col]) under the column kernel's
+// schedule for a grid of `grid` blocks (false: no compile-time plan)
+bool fft_cols_ct_owners(int height, int wf, int grid, std::vector<int>* owner);
 // tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built).
 // The row pass transforms the luma as is (sums unused): it does not wait for K1.
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
@@ -295,8 +316,8 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
                               unsigned long long* rsum = nullptr);
 // The column pass removes the DC bias (K1's channel sums) from column 0 first.
 // dbg (optional): the power spectrum, column-major [wf][height]
-hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const uint16_t* binmap,
-                              int nbins, unsigned long long* bin_sums, double* fmax_part, const double2* tw,
+hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const ColBins& cb,
+                              unsigned long long* bin_sums, double* fmax_part, const double2* tw,
                               const unsigned long long* sums, double* dbg, hipStream_t st);
 // Same, the luma from an fp64 plane when pgm != nullptr (planar input).
 hipError_t launch_sharpness_src(const uint8_t* img, const double* pgm, int height, int width, int n, const int* top,

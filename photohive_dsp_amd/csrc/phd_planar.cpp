@@ -150,11 +150,13 @@ Full_Report_Data* report_planar(Context* c, const double* r, const double* g, co
     }
     PHD_HIPN(hipEventSynchronize(c->ev[5]));
     const int hf = *(const int*)(h.data() + R.flags);
-    if (hf & 2 || hf & 4) {
+    if (hf & (2 | 4 | 8)) {
         (void)hipStreamSynchronize(st);
         set_error(hf & 2 ? "Error: channel values must be finite (NaN or infinity in the image)."
-                         : "Error: channel values above 1 put pixels outside the octree (out-of-bounds group in "
-                           "arm_octree).");
+                  : hf & 4 ? "Error: channel values above 1 put pixels outside the octree (out-of-bounds group in "
+                             "arm_octree)."
+                           : "Error: luma values outside [0, 1] (a pixel downsample_rgb does not sample); this "
+                             "library's polar-bin sums require channel values in [0, 1].");
         return nullptr;
     }
     // get_rgb_statistics: the partials in the order the device summed them

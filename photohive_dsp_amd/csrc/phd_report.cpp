@@ -374,11 +374,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const int nbins = cfg.radius_partitions * cfg.angle_partitions;
     const int ncrops = crops ? crops->N : 0;
     const int wf = width / 2 + 1;
-    FftSel fs;
-    if (!select_fft(c, height, width, nbins, d_imgs, n, &fs)) return false;
     const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
+    if (!tbl) return false;
+    FftSel fs;
+    if (!select_fft(c, height, width, nbins, d_imgs, n, &fs, tbl)) return false;
     const Context::Cls* cls = get_cls(c, gp);
-    if (!tbl || !cls) return false;
+    if (!cls) return false;
 
     const int ncolblocks = fs.col_blocks;
     // images whose result records go to the host together (one event and one
@@ -1159,10 +1160,10 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
     std::vector<const uint8_t*> imgs(n_images);
     for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
     const int nbins = cfg->radius_partitions * cfg->angle_partitions, wf = width / 2 + 1;
-    FftSel fs;
-    if (!select_fft(c, height, width, nbins, imgs.data(), n_images, &fs)) return -1;
     const BlurTable* tbl = get_table(c, height, width, cfg->radius_partitions, cfg->angle_partitions);
     if (!tbl) return -1;
+    FftSel fs;
+    if (!select_fft(c, height, width, nbins, imgs.data(), n_images, &fs, tbl)) return -1;
     // per image: bins, max partials, channel sums (+ the statistics pass's chunk slots)
     const long npix = (long)height * width;
     const int nchunks = (int)((npix + kChunk - 1) / kChunk);
@@ -1485,7 +1486,7 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
     const int wf = width / 2 + 1;
     const BlurTable* tbl = get_table(c, height, width, cfg->radius_partitions, cfg->angle_partitions);
     FftSel fs;
-    if (!cls || !tbl || !select_fft(c, height, width, cfg->radius_partitions * cfg->angle_partitions, &d_rgb, 1, &fs))
+    if (!cls || !tbl || !select_fft(c, height, width, cfg->radius_partitions * cfg->angle_partitions, &d_rgb, 1, &fs, tbl))
         return -1;
     // scratch outputs in the (large enough) workspace of the report just run
     uint8_t* dw = (uint8_t*)c->d_ws;
@@ -1569,7 +1570,7 @@ extern "C" int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int wi
     const int nbins = cfg.radius_partitions * cfg.angle_partitions;
     const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
     FftSel fs;
-    if (!tbl || !select_fft(c, height, width, nbins, &d_rgb, 1, &fs)) return -1;
+    if (!tbl || !select_fft(c, height, width, nbins, &d_rgb, 1, &fs, tbl)) return -1;
     if (!fs.ct) {
         set_error("no compile-time FFT plan for this size");
         return -2;

@@ -28,8 +28,10 @@ constexpr int kPT = 256;
 
 // flags (device int): bit 0 some value is not k/255 (not an 8-bit image);
 // bit 1 a value is not finite; bit 2 a pixel's group index falls outside the
-// octree (values above 1: the reference indexes out of bounds)
-constexpr int kFlagNotU8 = 1, kFlagNonFinite = 2, kFlagGroupRange = 4;
+// octree (values above 1: the reference indexes out of bounds); bit 3 a luma
+// value outside [0, 1] (any pixel, sampled by downsample_rgb or not): the
+// polar bins' fixed point (bin_scale) assumes |pgm - avg| <= 1
+constexpr int kFlagNotU8 = 1, kFlagNonFinite = 2, kFlagGroupRange = 4, kFlagLumaRange = 8;
 
 __device__ __forceinline__ void flag_wave(int* flags, bool bad, int bit) {
     if (__any(bad) && lane_id() == 0) atomicOr(flags, bit);
@@ -74,16 +76,19 @@ __global__ __launch_bounds__(kPT) void k_planar_moments(PlanarSrc P, long n, dou
     double s[3] = {0.0, 0.0, 0.0};
     for (long i0 = (long)blockIdx.x * kPT; i0 < n; i0 += (long)gridDim.x * kPT) {
         const long i = i0 + threadIdx.x;
-        bool bad = false;
+        bool bad = false, out = false;
         if (i < n) {
             const double r = P.r[i], g = P.g[i], b = P.b[i];
             bad = !isfinite(r) || !isfinite(g) || !isfinite(b);
             s[0] += r;
             s[1] += g;
             s[2] += b;
-            pgm[i] = 0.299 * r + 0.587 * g + 0.114 * b;
+            const double y = 0.299 * r + 0.587 * g + 0.114 * b;
+            pgm[i] = y;
+            out = !(y >= -1e-12 && y <= 1.0 + 1e-12);          // (0.299 + 0.587 + 0.114 rounds above 1)
         }
         flag_wave(flags, bad, kFlagNonFinite);
+        flag_wave(flags, out, kFlagLumaRange);
     }
     for (int c = 0; c < 3; c++) {
         const double t = block_sum(s[c], red);

@@ -58,6 +58,38 @@ def test_struct_layouts_match_reference_binding():
     assert S.Full_Report_Data.average_saturation.offset == 32
 
 
+def _our_layout():
+    from photohive_dsp_amd import structures as S
+    from tests.golden.make_struct_layout import layout
+    return layout(S)
+
+
+def test_every_field_offset_matches_reference_structures():
+    """Every Structure of the reference's structures.py (its ctypes binding, the
+    drop-in contract): same fields in the same order, same offsets, sizes and
+    ctypes types.  Against the committed fixture (tests/golden/struct_layout.json,
+    written from the reference by tests/golden/make_struct_layout.py)."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "struct_layout.json")) as f:
+        ref = json.load(f)
+    ours = _our_layout()
+    for name, want in ref.items():
+        assert name in ours, f"{name} missing from photohive_dsp_amd/structures.py"
+        assert ours[name] == want, (name, ours[name], want)
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/structures.py"),
+                    reason="the reference tree exists only in the build container")
+def test_field_offsets_match_live_reference_structures():
+    """The same comparison against the reference's structures.py itself, loaded
+    by importlib (no other reference module is imported)."""
+    from tests.golden.make_struct_layout import layout, load_reference
+    ref = layout(load_reference())
+    ours = _our_layout()
+    for name, want in ref.items():
+        assert ours.get(name) == want, (name, ours.get(name), want)
+
+
 def test_config_defaults_match_get_report():
     from photohive_dsp_amd.lib import lib
     from photohive_dsp_amd.structures import PhdConfig

@@ -101,3 +101,18 @@ def test_planar_rejects_non_finite():
     img[10, 10, 1] = np.nan
     assert _call(img) is None
     assert "finite" in L.last_error()
+
+
+def test_planar_rejects_oversized_unsampled_value():
+    """downsample_rate 2: a huge finite value on a pixel downsample_rgb never
+    samples (odd column) reaches only the statistics and the FFT.  Its luma
+    breaks the polar bins' fixed-point bound (|pgm - avg| <= 1, bin_scale), so
+    the call is rejected with a message instead of returning wrapped sums."""
+    phd, L = _phd()
+    from photohive_dsp_amd import synth
+    img = synth.deep("uniform", 400, 400, 2)
+    ok = _call(img, {"downsample_rate": 2})
+    assert ok is not None
+    img[11, 11, 0] = 1e300                            # column 11: not sampled at ds = 2 (x * 2)
+    assert _call(img, {"downsample_rate": 2}) is None
+    assert "luma" in L.last_error()

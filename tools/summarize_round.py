@@ -26,7 +26,11 @@ def main():
         t = last_json(p)
         print("two_lanes", t["value"], t["two_lanes"]["images_per_s"])
     for f in ("prof2", "prof"):
-        for row in csv.DictReader(open(os.path.join(OUT, f, "prof_kernel_stats.csv"))):
+        path = os.path.join(OUT, f, "prof_kernel_stats.csv")
+        if not os.path.exists(path):
+            print(f, "no kernel statistics (", path, "missing )")
+            continue
+        for row in csv.DictReader(open(path)):
             if any(k in row["Name"] for k in ("k_cols_ct<3000", "k_rows_ct<4000", "k_k1t<512")):
                 print(f, row["Name"][30:52], row["Calls"], round(float(row["AverageNs"]) / 1e3, 2))
 
