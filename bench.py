@@ -48,9 +48,11 @@ def parse(argv=None):
                    help="library lanes for every config of the run (phd_set_lanes; the library's default is 1): "
                         "1 keeps each kernel launch alone on the GPU, so its event duration prices the kernel "
                         "(the roofline)")
-    p.add_argument("--no-two-lanes", dest="two_lanes", action="store_false",
-                   help="skip the extra two_lanes object: the headline workload over two library lanes "
-                        "(phd_set_lanes(2), the opt-in concurrent mode), images/s only")
+    p.add_argument("--two-lanes", action="store_true",
+                   help="also run the headline workload over two library lanes (phd_set_lanes(2), the opt-in "
+                        "concurrent mode) and report its images/s as two_lanes; off by default so that every "
+                        "kernel launch of the default command runs alone and its rocprofv3 statistics agree "
+                        "with the roofline")
     p.add_argument("--height", type=int, default=3000)
     p.add_argument("--width", type=int, default=4000)
     p.add_argument("--no-cpu-baseline", action="store_true")

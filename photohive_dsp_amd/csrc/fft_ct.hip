@@ -730,7 +730,7 @@ int cols_grid(int, int nbins) {
         int g = resident_grid(k_cols_glds<H, T, CPB, Rs...>, T, cols_lds<H, T, CPB, Rs...>(nbins));
         g = g / 32 * 32;                                    // XCD quads b, b^8, b^16, b^24
         return g < 32 ? 32 : g;
-    }
+    } else {
     int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
     if ((CPB & 3) == 2) {
         g = g / 16 * 16;                                    // XCD pairs b, b^8
@@ -738,6 +738,7 @@ int cols_grid(int, int nbins) {
     }
     g = g / 32 * 32;                                        // XCD quads b, b^8, b^16, b^24
     return g < 32 ? 32 : g;
+    }
 }
 
 template <int H, int T, int CPB, int... Rs>

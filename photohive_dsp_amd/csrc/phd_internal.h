@@ -281,6 +281,9 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 10, 256, 33, 15, 20, 10)   \
     X(3000, 11, 256, 33, 25, 12, 10)   \
     X(3000, 12, 256, 65, 15, 10, 20)   \
+    X(3000, 13, 512, 5, 6, 5, 10, 10)  \
+    X(3000, 14, 384, 5, 15, 20, 10)    \
+    X(3000, 15, 384, 5, 6, 5, 10, 10)  \
     X(6000, 0, 512, 5, 15, 20, 20)     \
     X(6000, 1, 512, 5, 10, 20, 30)     \
     X(4000, 0, 256, 5, 10, 20, 20)     \
