@@ -92,7 +92,7 @@ __global__ __launch_bounds__(T) void k_fft_rows(const uint8_t* __restrict__ img0
     }
 }
 
-// LDS: [ C*H complex | twiddles (64 + n_hi) | polar bins (nbins doubles, if lds_bins) ]
+// LDS: [ C*H complex | twiddles (64 + n_hi) | log_mant table | polar bins (nbins u64, if lds_bins) ]
 template <int T, bool GEN>
 __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inter0, size_t inter_stride, int H,
                                                 int wf, int C, FftPlan plan, const uint16_t* __restrict__ binmap,
@@ -107,12 +107,14 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* buf = reinterpret_cast<double2*>(smem);
     double2* tw = buf + (size_t)C * H;
-    unsigned long long* lb = reinterpret_cast<unsigned long long*>(tw + 64 + plan.n_hi);
+    double2* lt = tw + 64 + plan.n_hi;
+    unsigned long long* lb = reinterpret_cast<unsigned long long*>(lt + kLogTab);
     const int tid = threadIdx.x;
     const int cb = blockIdx.x;
     const int k0 = cb * C;
     const int nc = min(C, wf - k0);
     load_twiddles(tw, plan);
+    log_table_init(lt, tid, T);
     if (lds_bins)
         for (int i = tid; i < nbins; i += T) lb[i] = 0ull;
     {
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
             if (p >= 1) {                               // fft_processing.c:197-198
                 const int c = i / H, u = i - c * H;
                 b = binmap[(size_t)(k0 + c) * H + u];
-                lg = bin_fixed(log(p), bscale);
+                lg = bin_fixed(log_mant(p, lt), bscale);
             }
         }
         // fixed-point integers: the sums do not depend on the atomics' order
@@ -231,7 +233,7 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     constexpr size_t kLdsBudget = 158 * 1024;
     const size_t bins_bytes = sizeof(unsigned long long) * nbins;
     const int lds_bins = bins_bytes <= 48 * 1024;
-    const size_t fixed = sizeof(double2) * (64 + plan.n_hi) + (lds_bins ? bins_bytes : 0);
+    const size_t fixed = sizeof(double2) * (64 + plan.n_hi + kLogTab) + (lds_bins ? bins_bytes : 0);
     const size_t col_bytes = sizeof(double2) * height;
     int C = 1;
     while (C < 8 && (size_t)(2 * C) * height <= (size_t)kFftMaxLds && (2 * C) * col_bytes + fixed <= kLdsBudget)

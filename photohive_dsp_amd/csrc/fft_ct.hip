@@ -81,9 +81,9 @@ __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
 // unrolled walk ran it on almost every row (some lane of 64 changes bin there).
 template <int E>
 __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0, int rend, const unsigned* bmw,
-                                          unsigned long long* bsum, double bscale) {
+                                          unsigned long long* bsum, double bscale, const double2* __restrict__ lt) {
     auto flush = [&](int b, double m, int e) {
-        const double acc = fmax((double)e * 0.69314718055994530942 + log(m), 0.0);
+        const double acc = fmax((double)e * 0.69314718055994530942 + log_mant(m, lt), 0.0);
         atomicAdd(&bsum[b], bin_fixed(acc, bscale));
     };
     int cur = -1, esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
@@ -307,7 +307,9 @@ struct ColK {
     static constexpr int NT = NC * T;                                     // block size
     static constexpr int CR = (2 * NC * P + NT - 1) / NT;                 // load rounds
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
-    static size_t lds(int nbins) { return sizeof(double2) * (NC * H + NTW) + (GB ? 0 : sizeof(unsigned long long) * nbins); }
+    static size_t lds(int nbins) {
+        return sizeof(double2) * (NC * H + NTW + kLogTab) + (GB ? 0 : sizeof(unsigned long long) * nbins);
+    }
     static_assert(Radices<Rs...>::product == H, "plan");
     // waves per SIMD of the launch bounds: one-column blocks are sized for two
     // resident blocks per CU, one when the column and twiddles fill the LDS
@@ -339,7 +341,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     double2* bufs = reinterpret_cast<double2*>(smem);         // [CPB][H]
     double2* tw = bufs + NC * H;
-    unsigned long long* lb = reinterpret_cast<unsigned long long*>(tw + K::NTW);
+    double2* lt = tw + K::NTW;                                 // log_mant's table
+    unsigned long long* lb = reinterpret_cast<unsigned long long*>(lt + kLogTab);
     const int tid = threadIdx.x;
     // NC == 1: blocks b, b^8, b^16, b^24 (one XCD) take the four columns of a
     // 128-byte line (two tiles), so each line is fetched once into that L2
@@ -351,6 +354,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     for (int i = tid; i < K::NTW; i += NT) tw[i] = twg[i];
     if (!K::GB)
         for (int i = tid; i < nbins; i += NT) lb[i] = 0ull;
+    log_table_init(lt, tid, NT);
     unsigned long long* const bsum = K::GB ? bin_sums : lb;   // where the runs are added
     const int kpn = (wf + 1) / 2;
     const int nunit = (kpn + 1) / 2;                          // tile pairs (128-byte lines)
@@ -486,7 +490,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
-        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, bmw, bsum, bscale);
+        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, bmw, bsum, bscale, lt);
         __syncthreads();
     }
 #undef PHD_COL_FETCH
@@ -533,7 +537,8 @@ struct GlK {
     static constexpr int NGW = (NG + T / 64 - 1) / (T / 64);  // ... per wave
     static constexpr size_t off_lgb = sizeof(double2) * H;
     static constexpr size_t off_tw = off_lgb + sizeof(double) * HH;
-    static constexpr size_t off_bins = off_tw + sizeof(double2) * NTW;
+    static constexpr size_t off_lt = off_tw + sizeof(double2) * NTW;
+    static constexpr size_t off_bins = off_lt + sizeof(double2) * kLogTab;
     static size_t lds(int nlb) { return off_bins + sizeof(unsigned long long) * nlb; }
     static_assert(T % 64 == 0 && HH % 2 == 0 && E % 2 == 0, "whole waves; even halves (dword bin-id loads)");
     static_assert(Radices<Rs...>::product == H, "plan");
@@ -566,6 +571,8 @@ __global__ __launch_bounds__(T, T / 128) void k_cols_glds(
     const int tid = threadIdx.x;
     for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
     for (int i = tid; i < nlb; i += T) lb[i] = 0ull;
+    double2* lt = reinterpret_cast<double2*>(smem + K::off_lt);
+    log_table_init(lt, tid, T);
     // k_cols_ct's schedule (cols_owners): quad q = (b >> 3) & 3 of an XCD takes
     // column 2 (2 u + q / 2) + q % 2 of each of its 128-byte lines u
     const int kpn = (wf + 1) / 2, nunit = (kpn + 1) / 2;
@@ -672,7 +679,7 @@ __global__ __launch_bounds__(T, T / 128) void k_cols_glds(
             }
             __syncthreads();
             // contiguous runs of one bin, one LDS atomic per run (walk_runs)
-            walk_runs<E>(lgb, tid * E, HH, bmw[h2], lb, bscale);
+            walk_runs<E>(lgb, tid * E, HH, bmw[h2], lb, bscale, lt);
             __syncthreads();
         }
     }
