@@ -708,6 +708,9 @@ int resident_grid(K kernel, int threads, size_t lds) {
     allow_big_lds(kernel);
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess || nb < 1) nb = 1;
+    // PHD_FFT_BPC (experiment): at most this many persistent blocks per CU
+    static const int cap = getenv("PHD_FFT_BPC") ? atoi(getenv("PHD_FFT_BPC")) : 0;
+    if (cap > 0 && nb > cap) nb = cap;
     return nb * num_cus();
 }
 

@@ -561,7 +561,9 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                      (cshift < 0 || 19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus));
     if (two) {                                            // two 512-thread blocks per CU
         const size_t lds = (size_t)t_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
-        const int grid = (int)std::min<long>(nitems, 2L * num_cus());
+        // with two lanes, one block per CU: the other half of each CU stays free
+        // for the other lane's FFT blocks (k1_blocks_per_cu)
+        const int grid = (int)std::min<long>(nitems, (long)k1_blocks_per_cu() * num_cus());
         phd_launch((k_k1t<512, true>), dim3(grid), dim3(512), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255,
                    out0, a_stride, h_stride, cshift2, g_ablate | env_ablate());
     } else {                                              // one 1024-thread block per CU

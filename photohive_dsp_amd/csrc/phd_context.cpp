@@ -161,6 +161,11 @@ int lanes_setting() {
     return l;
 }
 
+int k1_blocks_per_cu() {
+    static const int env = getenv("PHD_K1_BPC") ? std::max(1, std::min(2, atoi(getenv("PHD_K1_BPC")))) : 0;
+    return env ? env : (lanes_setting() >= 2 ? 1 : 2);
+}
+
 LaneWorker* lane_worker() {
     // one per process (a forked child has none of its parent's threads)
     static std::mutex m;

@@ -141,6 +141,11 @@ struct FftPlan {
 extern int g_ablate;   // ablation mask read by kernels under phd_debug_time_kernel
 int env_ablate();      // PHD_ABLATE (timing builds only)
 int num_cus();         // compute units of the current device
+// K1's two-block form: blocks per CU (2; 1 when device batches run on two
+// lanes, so a K1 launch leaves half of every CU to the other lane's FFT
+// blocks: 7.89k against 7.66k images/s with two lanes, and 6.78k against
+// 7.07k with one, where K1 runs alone; PHD_K1_BPC overrides)
+int k1_blocks_per_cu();
 // hsv/stats/histogram pass over one image (K1).  ds = downsample rate.
 // K1 over a batch of same-size images (ds == 1); d_imgs is a device array of
 // n image pointers; image i's records sit at out0 + i * a_stride (sums, hist,
