@@ -806,7 +806,22 @@ void cols_owners(int wf, int grid, std::vector<int>* owner) {
     } while (0)
 #define PHD_HAVE(N, V, T, ...) if (n_ == N && V == want_) have_ = true;
 
+// log_mant over an array (tests: its accuracy against the host's log)
+__global__ __launch_bounds__(256) void k_log_mant(const double* __restrict__ x, double* __restrict__ y, long n) {
+    __shared__ double2 lt[kLogTab];
+    log_table_init(lt, threadIdx.x, 256);
+    __syncthreads();
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) y[i] = log_mant(x[i], lt);
+}
+
 }  // namespace
+
+hipError_t launch_log_mant(const double* x, double* y, long n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    phd_launch(k_log_mant, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, y, n);
+    return hipGetLastError();
+}
 
 int ct_variant(bool rows) {
     static const int vr = getenv("PHD_CT_ROWS_VARIANT") ? atoi(getenv("PHD_CT_ROWS_VARIANT")) : 0;

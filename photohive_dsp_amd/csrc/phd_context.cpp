@@ -317,8 +317,13 @@ const double2* get_ct_twiddles(Context* c, int n, bool rows) {
 // a CU than the full table does (measured: at the same occupancy the full
 // table is the faster, 55.7 against 60.0 us at 4000x3000; 4000-row columns at
 // two blocks per CU instead of one, 103.6 against 143.3 us).
+int col_windows_mode(int set) {
+    static std::atomic<int> mode{getenv("PHD_COL_WINDOWS") ? atoi(getenv("PHD_COL_WINDOWS")) : 1};
+    return set >= 0 ? mode.exchange(set) : mode.load();
+}
+
 static const ColWin* get_col_windows(Context* c, const BlurTable& t, int width) {
-    static const int mode = getenv("PHD_COL_WINDOWS") ? atoi(getenv("PHD_COL_WINDOWS")) : 1;   // 0 off, 2 always
+    const int mode = col_windows_mode(-1);                  // 0 off, 1 where they raise occupancy, 2 always
     if (mode == 0) return nullptr;
     const int nbins = t.na * t.nr;
     const int g_full = fft_cols_ct_blocks(t.height, t.wf, nbins);

@@ -312,6 +312,11 @@ struct ColBins {
     int grid = 0;                    // the grid the windows were made for (0: from occupancy)
 };
 size_t fft_cols_ct_lds(int height, int nlb);
+// log_mant (phd_device.h) over n positive doubles (tests)
+hipError_t launch_log_mant(const double* x, double* y, long n, hipStream_t st);
+// the column-pass bin windows: 0 off, 1 where they raise occupancy (default),
+// 2 always; -1 leaves PHD_COL_WINDOWS / the default (phd_debug_col_windows)
+int col_windows_mode(int set);
 // persistent grid of the column kernel (= entries of fmax_part) with nlb LDS bins
 int fft_cols_ct_blocks(int height, int wf, int nlb);
 // the block that processes each column (owner[col]) under the column kernel's

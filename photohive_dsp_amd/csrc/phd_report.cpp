@@ -1556,6 +1556,22 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
 // the production FFT kernels (compile-time plans only), column-major into
 // d_out[(W/2+1) * H] (device).  Returns 0, -2 when the size has no
 // compile-time plan, or -1.
+extern "C" int phd_debug_log_mant(const double* d_x, double* d_y, long n) {
+    clear_error();
+    Context* c = get_context();
+    if (!c) return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipError_t e = launch_log_mant(d_x, d_y, n, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        set_error(std::string("phd_debug_log_mant: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+extern "C" int phd_debug_col_windows(int mode) { return col_windows_mode(mode); }
+
 extern "C" int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int width, double* d_out) {
     clear_error();
     Context* c = get_context();

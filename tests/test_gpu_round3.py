@@ -1,0 +1,59 @@
+"""Round-3 device pieces: the polar bins' table-driven fp64 log (log_mant) and
+the column pass's per-block bin windows (ColBins).  Every call goes through the
+C-ABI (photohive_dsp_amd.lib)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    import torch
+    from photohive_dsp_amd import lib as L
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return L, torch
+
+
+def test_log_mant_matches_host_log():
+    """log_mant (phd_device.h) against numpy's log over the values the column
+    passes take it of: mantissa products of up to 16 factors in [1/2, 1) and
+    single powers p in [1, N^2] (the runtime-plan pass), plus the edges of the
+    table's 32 intervals.  Within 4e-16 * max(1, |log x|) absolute (a few ulp;
+    the bins are fixed point at 2^-30 .. 2^-41 per run)."""
+    L, torch = _lib()
+    rng = np.random.default_rng(3)
+    prods = np.prod(rng.uniform(0.5, 1.0, (200_000, 16)), axis=1)
+    powers = 10.0 ** rng.uniform(0.0, 15.0, 200_000)
+    edges = np.concatenate([1.0 + np.arange(33) / 32.0, np.nextafter(1.0 + np.arange(1, 33) / 32.0, 0.0)]) / 2.0
+    x = np.concatenate([prods, powers, edges, [1.0, 0.5, 2.0 ** -40, 1.4e14]])
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.empty_like(dx)
+    assert L.lib.phd_debug_log_mant(dx.data_ptr(), dy.data_ptr(), x.size) == 0, L.last_error()
+    y = dy.cpu().numpy()
+    want = np.log(x)
+    err = np.abs(y - want) / np.maximum(1.0, np.abs(want))
+    assert err.max() <= 4e-16, (err.max(), x[np.argmax(err)])
+
+
+@pytest.mark.parametrize("shape", [(4000, 6000), (3000, 4000)])
+def test_column_bin_windows_bit_identical(shape):
+    """The per-block LDS windows of polar bins sum the same fixed-point run values
+    into the same bins as the full table: bins and vectors bit-identical with the
+    windows off, where the occupancy rule turns them on (4000-row columns) and
+    forced (3000-row columns)."""
+    L, torch = _lib()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import blur_profiles_device
+    h, w = shape
+    imgs = torch.from_numpy(np.stack([synth.make("structured", h, w, 21), synth.uniform(h, w, 22)])).cuda()
+    prev = L.lib.phd_debug_col_windows(0)
+    try:
+        off_bins, off_vecs = blur_profiles_device(imgs)
+        L.lib.phd_debug_col_windows(2)
+        on_bins, on_vecs = blur_profiles_device(imgs)
+    finally:
+        L.lib.phd_debug_col_windows(prev)
+    assert np.array_equal(on_bins, off_bins)
+    assert on_vecs == off_vecs
