@@ -507,195 +507,6 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     if (!K::GB && !(ablate & 8)) flush_bins(lb, nbins, win, nr, bin_sums, tid, NT);
 }
 
-// ---- column pass, LDS-DMA form (CPB flag 64) ---------------------------------
-//
-// The k_cols_ct schedule (one column per block of T threads, blocks b, b^8,
-// b^16, b^24 of an XCD taking the four columns of the same 128-byte lines, two
-// blocks per CU), with the NEXT COLUMN STREAMED INTO LDS WHILE THE CURRENT ONE
-// FINISHES: as soon as every thread holds its last-pass inputs in registers the
-// column buffer is free, and each wave issues global_load_lds_dwordx4 (64 rows
-// x 16 B per instruction, written lane-linear into the buffer: no VGPRs, no
-// ds_write).  The last pass, p = re^2 + im^2, the max and the run binning of the
-// current column then run while the loads are in flight; the loop head waits
-// for them (vmcnt) and a barrier publishes them.  k_cols_ct instead issues a
-// column's loads at the start of its step and waits for them at once.
-//
-// LDS: the column (16 H), p per row for one half of the rows (8 ceil(H/2): the
-// walk runs over the two halves in turn, so the column buffer is free for the
-// next column's rows), the twiddles and the block's window of polar bins
-// (ColBins): at H = 3000 and 72 x 40 bins 48 + 12 + 2.6 + <= 14.2 KB, two blocks
-// per CU.
-template <int H, int T, int CPB, int... Rs>
-struct GlK {
-    using PL = Plan<H, T, 1, Rs...>;
-    using L = typename PL::Last;
-    static constexpr int R = H / L::NB;                       // last radix
-    static constexpr int NTW = tw_entries<1, Rs...>();
-    static constexpr int HH = (H + 1) / 2;                    // rows per walk half
-    static constexpr int E = (HH + T - 1) / T;                // walk rows per thread per half
-    static constexpr int NG = (H + 63) / 64;                  // LDS-DMA instructions per column
-    static constexpr int NGW = (NG + T / 64 - 1) / (T / 64);  // ... per wave
-    static constexpr size_t off_lgb = sizeof(double2) * H;
-    static constexpr size_t off_tw = off_lgb + sizeof(double) * HH;
-    static constexpr size_t off_lt = off_tw + sizeof(double2) * NTW;
-    static constexpr size_t off_bins = off_lt + sizeof(double2) * kLogTab;
-    static size_t lds(int nlb) { return off_bins + sizeof(unsigned long long) * nlb; }
-    static_assert(T % 64 == 0 && HH % 2 == 0 && E % 2 == 0, "whole waves; even halves (dword bin-id loads)");
-    static_assert(Radices<Rs...>::product == H, "plan");
-};
-
-// one wave's 64 x 16 B: lane l's source `src` lands at LDS byte address
-// lds_dst + 16 l (M0 is written and restored in the same statement)
-__device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds_dst)
-                 : "memory");
-}
-
-template <int H, int T, int CPB, int... Rs>
-__global__ __launch_bounds__(T, T / 128) void k_cols_glds(
-    const double2* __restrict__ inter, int wf, const uint16_t* __restrict__ binmap, int nlb,
-    const int* __restrict__ win, int nr,
-    unsigned long long* __restrict__ bin_sums, double* __restrict__ fmax_part, const double2* __restrict__ twg,
-    const unsigned long long* __restrict__ sums, int width, double* __restrict__ dbg, double bscale) {
-    using K = GlK<H, T, CPB, Rs...>;
-    using L = typename K::L;
-    constexpr int R = K::R, E = K::E, HH = K::HH;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double2* buf = reinterpret_cast<double2*>(smem);
-    double* lgb = reinterpret_cast<double*>(smem + K::off_lgb);
-    double2* tw = reinterpret_cast<double2*>(smem + K::off_tw);
-    unsigned long long* lb = reinterpret_cast<unsigned long long*>(smem + K::off_bins);
-    const int tid = threadIdx.x;
-    for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
-    for (int i = tid; i < nlb; i += T) lb[i] = 0ull;
-    double2* lt = reinterpret_cast<double2*>(smem + K::off_lt);
-    log_table_init(lt, tid, T);
-    // k_cols_ct's schedule (cols_owners): quad q = (b >> 3) & 3 of an XCD takes
-    // column 2 (2 u + q / 2) + q % 2 of each of its 128-byte lines u
-    const int kpn = (wf + 1) / 2, nunit = (kpn + 1) / 2;
-    const int quad = (int)((blockIdx.x >> 3) & 3), half = quad & 1;
-    const int nlog = (int)gridDim.x / 4;
-    const int lblk = (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
-    const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
-    auto pair_at = [&](int u) { return min(2 * u + (quad >> 1), kpn - 1); };
-    const unsigned lds_buf = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(buf));
-    const int wv = tid >> 6, ln = tid & 63;
-    // the column (half `half` of tile kp) into the buffer: wave w issues
-    // instructions w, w + T/64, ... (rows 64 i + lane), rows past H masked off
-    auto stream_in = [&](int kp) {
-        const double2* src = inter + ((size_t)kp * 2 + half) * 2 + (size_t)((64 * wv + ln) >> 1) * kpn * 4 + (ln & 1);
-        const size_t step = (size_t)(T / 2) * kpn * 4;       // T rows = T / 2 row pairs per instruction step
-#pragma unroll
-        for (int j = 0; j < K::NGW; j++) {
-            const int i = wv + j * (T / 64);
-            if (i < K::NG && 64 * i + ln < H)
-                glds16(src, __builtin_amdgcn_readfirstlane(lds_buf + (unsigned)(64 * i) * 16u));
-            src += step;
-        }
-    };
-    if (c0 < c1) stream_in(pair_at(c0));
-    double mx = 0.0;
-    for (int u = c0; u < c1; u++) {
-        const int kp = pair_at(u);
-        const int col = 2 * (2 * u + (quad >> 1)) + half;     // unclamped: past the last tile idles
-        const bool live = col < wf;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the streamed column has landed
-        __syncthreads();
-        // this thread's bin ids: rows tid E .. tid E + E - 1 of each half (issued
-        // after the wait above, so they are in flight during the passes)
-        unsigned bmw[2][E / 2];
-        {
-            const uint16_t* bcol = binmap + (size_t)(live ? col : 0) * H + tid * E;
-            const bool any = tid * E < HH;                    // threads past the half's end walk nothing
-#pragma unroll
-            for (int h2 = 0; h2 < 2; h2++)
-#pragma unroll
-                for (int j = 0; j < E / 2; j++)
-                    bmw[h2][j] = any ? reinterpret_cast<const unsigned*>(bcol + h2 * HH)[j] : 0u;
-        }
-        if (kp == 0) {                                        // block-uniform
-            // remove_dc_bias (src/blur_profile.c:233-238) on column 0 (see k_cols_ct)
-            if (col == 0) {
-                const double n = (double)H * (double)width;
-                const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
-                                    (double)sums[2] / 255.0 / n) / 3.0;
-                const double dc = (double)width * avg;
-                for (int y = tid; y < H; y += T) buf[y].x -= dc;
-            }
-            __syncthreads();
-        }
-        K::PL::all_but_last(buf, tw, tid);
-        double2 v[L::ROUNDS][R];
-        L::load(buf, v, tid);
-        // the bin ids are consumed here, before the next column's loads are issued
-        // (a plain load's first use waits for every vector-memory operation)
-#pragma unroll
-        for (int h2 = 0; h2 < 2; h2++)
-#pragma unroll
-            for (int j = 0; j < E / 2; j++) asm volatile("" ::"v"(bmw[h2][j]));
-        __syncthreads();                                      // every thread holds its inputs: buffer free
-        if (u + 1 < c1) stream_in(pair_at(u + 1));
-        L::compute(v, tw + K::PL::last_tw_offset, tid);
-        // p per output; rows of the first half go to LDS at once, the second
-        // half's stay in registers until the first half has been walked (row
-        // b + k NB is in the first half for k < KH when NB divides HH)
-        constexpr bool SPLITK = L::ROUNDS == 1 && HH % L::NB == 0;
-        constexpr int KH = SPLITK ? HH / L::NB : R;
-        double pw[L::ROUNDS][R];
-#pragma unroll
-        for (int q = 0; q < L::ROUNDS; q++) {
-            const int b = tid + q * T;
-            if (L::active(b)) {
-#pragma unroll
-                for (int k = 0; k < R; k++) {
-                    const double2 X = v[q][k];
-                    const double p = X.x * X.x + X.y * X.y;          // src/fft_processing.c:49
-                    if (live) mx = fmax(mx, p);
-                    if (dbg && live) dbg[(size_t)col * H + b + k * L::NB] = p;
-                    const double pc = (live && p >= 1) ? p : 1.0;   // src/fft_processing.c:197-198
-                    if (SPLITK && k < KH) lgb[b + k * L::NB] = pc;
-                    else pw[q][k] = pc;
-                }
-            }
-        }
-#pragma unroll
-        for (int h2 = 0; h2 < 2; h2++) {
-            if (!SPLITK || h2 == 1) {
-                // p of the half's rows to LDS (tested per element unless SPLITK)
-#pragma unroll
-                for (int q = 0; q < L::ROUNDS; q++) {
-                    const int b = tid + q * T;
-                    if (L::active(b)) {
-#pragma unroll
-                        for (int k = SPLITK ? KH : 0; k < R; k++) {
-                            const int y = b + k * L::NB;
-                            if (SPLITK || (y >= HH) == (h2 == 1)) lgb[y - h2 * HH] = pw[q][k];
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            // contiguous runs of one bin, one LDS atomic per run (walk_runs)
-            walk_runs<E>(lgb, tid * E, HH, bmw[h2], lb, bscale, lt);
-            __syncthreads();
-        }
-    }
-    // block max -> one partial per block; non-zero bins -> the image's sums
-    mx = wave_max(mx);
-    double* red = lgb;
-    if (lane_id() == 0) red[tid >> 6] = mx;
-    __syncthreads();
-    if (tid == 0) {
-        double m = 0.0;
-        for (int w = 0; w < T / 64; w++) m = fmax(m, red[w]);
-        fmax_part[blockIdx.x] = m;
-    }
-    flush_bins(lb, nlb, win, nr, bin_sums, tid, T);
-}
-
 template <typename K>
 void allow_big_lds(K kernel) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -730,17 +541,11 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
 // column-pass LDS bytes of a plan (CPB flag 64: the LDS-DMA form)
 template <int H, int T, int CPB, int... Rs>
 size_t cols_lds(int nbins) {
-    if constexpr ((CPB & 64) != 0) return GlK<H, T, CPB, Rs...>::lds(nbins);
-    else return ColK<H, T, CPB, Rs...>::lds(nbins);
+    return ColK<H, T, CPB, Rs...>::lds(nbins);
 }
 
 template <int H, int T, int CPB, int... Rs>
 int cols_grid(int, int nbins) {
-    if constexpr ((CPB & 64) != 0) {
-        int g = resident_grid(k_cols_glds<H, T, CPB, Rs...>, T, cols_lds<H, T, CPB, Rs...>(nbins));
-        g = g / 32 * 32;                                    // XCD quads b, b^8, b^16, b^24
-        return g < 32 ? 32 : g;
-    } else {
     int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
     if ((CPB & 3) == 2) {
         g = g / 16 * 16;                                    // XCD pairs b, b^8
@@ -748,7 +553,6 @@ int cols_grid(int, int nbins) {
     }
     g = g / 32 * 32;                                        // XCD quads b, b^8, b^16, b^24
     return g < 32 ? 32 : g;
-    }
 }
 
 template <int H, int T, int CPB, int... Rs>
@@ -757,12 +561,8 @@ hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, u
                    hipStream_t st) {
     const size_t lds = cols_lds<H, T, CPB, Rs...>(cb.nlb);
     const int grid = cb.grid > 0 ? cb.grid : cols_grid<H, T, CPB, Rs...>(wf, cb.nlb);
-    if constexpr ((CPB & 64) != 0)
-        phd_launch((k_cols_glds<H, T, CPB, Rs...>), dim3(grid), dim3(T), lds, st, inter, wf, cb.map, cb.nlb, cb.win,
-                   cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf));
-    else
-        phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.map, cb.nlb,
-                   cb.win, cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate);
+    phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.map, cb.nlb,
+               cb.win, cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate);
     return hipGetLastError();
 }
 
@@ -773,7 +573,7 @@ template <int H, int T, int CPB, int... Rs>
 void cols_owners(int wf, int grid, std::vector<int>* owner) {
     owner->assign(wf, -1);
     const int kpn = (wf + 1) / 2, nunit = (kpn + 1) / 2;
-    const bool pairs = (CPB & 64) == 0 && (CPB & 3) == 2;
+    const bool pairs = (CPB & 3) == 2;
     for (int b = 0; b < grid; b++) {
         const int q = pairs ? (b >> 3) & 1 : (b >> 3) & 3;
         const int nlog = pairs ? grid / 2 : grid / 4;

@@ -270,8 +270,11 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 // Round 3: columns of 4000 at 256 threads 143 us with the full bin table (one
 // block per CU by LDS), 104 us with per-block bin windows (two blocks per CU,
 // ColBins), against 159-162 us at 320 threads: 256 threads is variant 0.
-// Variant 12 (flag 64): k_cols_glds, the next column streamed into LDS by
-// LDS-DMA during the current one's last pass and binning (needs the windows).
+// Measured and removed in round 3: an LDS-DMA form
+// that streams the next column into LDS during the current column's last pass
+// (one column per block with bin windows: 55.9-58.6 against 54.9-56.8 us; two
+// columns per block in lockstep 75 us); plans of 3000 at 384 / 512 threads
+// (5 6 5 10 10, 15 20 10: 69.7-91 us).
 #define PHD_CT_COLS(X)                 \
     X(3000, 0, 256, 5, 15, 10, 20)     \
     X(3000, 1, 384, 2, 5, 6, 10, 10)   \
@@ -285,10 +288,6 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 9, 256, 33, 15, 10, 20)    \
     X(3000, 10, 256, 33, 15, 20, 10)   \
     X(3000, 11, 256, 33, 25, 12, 10)   \
-    X(3000, 12, 256, 65, 15, 10, 20)   \
-    X(3000, 13, 512, 5, 6, 5, 10, 10)  \
-    X(3000, 14, 384, 5, 15, 20, 10)    \
-    X(3000, 15, 384, 5, 6, 5, 10, 10)  \
     X(6000, 0, 512, 5, 15, 20, 20)     \
     X(6000, 1, 512, 5, 10, 20, 30)     \
     X(4000, 0, 256, 5, 10, 20, 20)     \
