@@ -513,6 +513,18 @@ __device__ __forceinline__ int exact_group_t(int kr, int kg, int kb, const ClsEn
     return g;
 }
 
+// Is the pixel's exact group g?  Integer work for all but a pixel on a hue-bin
+// edge whose candidate groups (classify_e's gcol, one hue bin below) include g.
+template <bool kThr>
+__device__ __forceinline__ bool in_group(int kr, int kg, int kb, int g, const ClsEnt* ent, const signed char* si8,
+                                         const double* k255, const GridParams& gp, const FastCls& fc) {
+    int hN, hD, gc;
+    const int q = classify_e<kThr>(kr, kg, kb, ent[max(kr, max(kg, kb))], si8, gp, fc, hN, hD, gc);
+    if (q != -2) return q == g;
+    if (gc != g && gc - gp.sp * gp.vp != g) return false;
+    return edge_group<kThr>(kr, kg, kb, hue_exact(kr, kg, kb, k255), ent, si8, gp) == g;
+}
+
 // Kcut for downsample_rate == 1, all images of a batch in one launch: one block
 // per (image, group) whose keep rule needs raster positions (the tie path of
 // group_irregular_pixels appends pixels in raster order until the parent's tail
@@ -583,8 +595,7 @@ __global__ __launch_bounds__(kK1Threads, 4) void k_cutoffs_b(
                 } else {
                     continue;
                 }
-                double sv;
-                if (exact_group_t<kThr>(kr, kg, kb, ent, si8, k255, gp, fc, sv) == g) hits |= 1u << (4 * st + i);
+                if (in_group<kThr>(kr, kg, kb, g, ent, si8, k255, gp, fc)) hits |= 1u << (4 * st + i);
             }
         }
         if (tid == 0) *found = 0;
@@ -869,8 +880,8 @@ __global__ __launch_bounds__(kPartThreads) void k_partial_sums_b(
     const long full_end = npix & ~3L;
     double th = 0.0, ts = 0.0, tv = 0.0, tn = 0.0;
     auto add = [&](int kr, int kg, int kb) {
-        double sv;
-        if (exact_group_t<kThr>(kr, kg, kb, ent, si8, k255, gp, fc, sv) != g) return;
+        if (!in_group<kThr>(kr, kg, kb, g, ent, si8, k255, gp, fc)) return;
+        const double sv = sat_of(max(kr, max(kg, kb)), min(kr, min(kg, kb)));
         double tp = hue_exact(kr, kg, kb, k255) + off;
         tp = tp > 360 ? tp - 360 : (tp < 0 ? tp + 360 : tp);
         th += tp;
@@ -1002,43 +1013,93 @@ __global__ __launch_bounds__(kPartThreads) void k_partial_sums_img(
         atomicAdd(&acc[4 * e + 2], v_of(max(kr, max(kg, kb)), k255));
         atomicAdd(&acc[4 * e + 3], 1.0);
     };
+    // a pixel by its exact group (the deferred and the unaligned tail pixels)
     auto add = [&](long p, int kr, int kg, int kb) {
         double sv;
         const int g = exact_group_t<kThr>(kr, kg, kb, ent, si8, k255, gp, fc, sv);
         const int e = g >= 0 ? gent[g] : -1;
         if (e >= 0 && p < (long)ecut[e]) put(e, kr, kg, kb, sv);
     };
+    // The walk classifies every pixel of the prefix to find the few of the
+    // partial groups, so the common case is all integer work: the group from
+    // classify_e (no saturation, no fp64); a pixel on a hue-bin edge (-2) is
+    // resolved exactly only when one of its two candidate groups (hue bins hi
+    // and hi - 1, gcol) is an entry, after the unit (a wave would otherwise run
+    // the fp64 hue for a pixel of one of its lanes on most steps).
+    const int svp = gp.sp * gp.vp;
     constexpr int kUnit = 16 * kPartThreads;
     const long full_end = npix & ~3L;
     const long umax = cmax > 0 ? (long)(cmax - 1) / kUnit : -1;
-    for (long u = blockIdx.y; u <= umax; u += gridDim.y) {
-        // block-uniform: skip a unit no entry needs (past its cutoff or none of its pixels in the chunk)
-        const long ub = u * kUnit, ch = ub / kChunk;
-        bool any = false;
-        for (int e = 0; e < ne; e++) any |= ub < (long)ecut[e] && chunk_hist[ch * tl + egrp[e]] != 0;
-        if (!any) continue;
-        const long end = std::min<long>(ub + kUnit, (long)cmax);
+    const int lane = lane_id();
+    // one unit: 16 pixels per thread (4 groups of 4, loaded together) and, in
+    // lane l < ne, entry l's pixel count in the unit's chunk (the skip test)
+    struct Unit {
         unsigned w[4][3];
-        bool okg[4];
+        bool ok[4];
+        unsigned hv;
+    };
+    auto fetch = [&](long u, Unit& x) {
+        const long ub = u * kUnit;
+        x.hv = lane < ne ? chunk_hist[(ub / kChunk) * tl + egrp[lane]] : 0u;
 #pragma unroll
         for (int st = 0; st < 4; st++) {
             const long p0 = ub + 4L * tid + 4L * kPartThreads * st;
-            okg[st] = p0 + 3 < full_end;
-            load_group<kAligned>(ip, p0, okg[st], w[st]);
+            x.ok[st] = p0 + 3 < full_end;
+            load_group<kAligned>(ip, p0, x.ok[st], x.w[st]);
         }
+    };
+    auto process = [&](long u, const Unit& x) {
+        // wave-uniform: skip a unit no entry needs (past its cutoff or none of
+        // its group's pixels in the chunk)
+        const long ub = u * kUnit;
+        if (__ballot(lane < ne && ub < (long)ecut[lane] && x.hv != 0u) == 0ull) return;
+        const long end = std::min<long>(ub + kUnit, (long)cmax);
+        unsigned cand = 0;                                   // bit 4 st + i: resolve exactly
 #pragma unroll
         for (int st = 0; st < 4; st++) {
             const long p0 = ub + 4L * tid + 4L * kPartThreads * st;
             if (p0 >= end) continue;
-            if (okg[st]) {
+            if (x.ok[st]) {
+                int g[4], gc[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (p0 + i < end)
-                        add(p0 + i, px_byte(w[st], 3 * i), px_byte(w[st], 3 * i + 1), px_byte(w[st], 3 * i + 2));
+                for (int i = 0; i < 4; i++) {
+                    const int kr = px_byte(x.w[st], 3 * i), kg = px_byte(x.w[st], 3 * i + 1),
+                              kb = px_byte(x.w[st], 3 * i + 2);
+                    int hN, hD;
+                    g[i] = classify_e<kThr>(kr, kg, kb, ent[max(kr, max(kg, kb))], si8, gp, fc, hN, hD, gc[i]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const bool c = g[i] >= 0 ? gent[g[i]] >= 0
+                                             : (gent[gc[i]] >= 0 || (gc[i] >= svp && gent[gc[i] - svp] >= 0));
+                    cand |= (unsigned)(c && p0 + i < end) << (4 * st + i);
+                }
             } else {
                 for (long p = p0; p < p0 + 4 && p < end && p < npix; p++) add(p, ip[3 * p], ip[3 * p + 1], ip[3 * p + 2]);
             }
         }
+        while (cand) {
+            const int bt = __ffs(cand) - 1;
+            cand &= cand - 1;
+            const int st = bt >> 2, i = bt & 3;
+            add(ub + 4L * tid + 4L * kPartThreads * st + i, px_byte(x.w[st], 3 * i), px_byte(x.w[st], 3 * i + 1),
+                px_byte(x.w[st], 3 * i + 2));
+        }
+    };
+    // two units in flight: the next one's loads are issued before this one's
+    // classification (the walk is otherwise bound by the load latency)
+    Unit ua, ub2;
+    const long gy = gridDim.y;
+    long u = blockIdx.y;
+    if (u <= umax) fetch(u, ua);
+    while (u <= umax) {
+        const long v = u + gy;
+        if (v <= umax) fetch(v, ub2);
+        process(u, ua);
+        if (v > umax) break;
+        u = v + gy;
+        if (u <= umax) fetch(u, ua);
+        process(v, ub2);
     }
     if (blockIdx.y == 0)
         for (int e = tid; e < ne; e += kPartThreads) {
@@ -1590,7 +1651,8 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     if (!per_group && max_per_image <= kPartImgMax && max_per_image > 1) {
         const size_t lds = PartImgLds::bytes(gp.tl);
         // (grid.y 16: same step time; 4: 4 % slower, the walks then outlast the FFTs they share the CUs with)
-        const dim3 grid(n, 64);
+        static const int gy = getenv("PHD_PART_GY") ? std::max(1, atoi(getenv("PHD_PART_GY"))) : 64;
+        const dim3 grid(n, gy);
 #define PHD_PI_LAUNCH(A, T)                                                                                     \
     phd_launch((k_partial_sums_img<A, T>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc, tabs, \
                        k255, entries, n_entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride)

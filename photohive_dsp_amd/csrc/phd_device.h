@@ -111,10 +111,12 @@ __device__ __forceinline__ int si_of(const ClsEnt& e, int kmx, int kd, const sig
 // Branch-free: bitwise ands and selects only.
 // Also returns hN and hD: rgb2hsv's hue is hN / hD exactly (hD = max - min,
 // or hN = 0, hD = 1 for a gray pixel), so a caller that needs h for sums gets it
-// from one reciprocal.
+// from one reciprocal, and gcol, the colour group of hue bin floor(N / D): for
+// a -2 pixel (on a bin edge) the exact group is gcol or the group one hue bin
+// below (the reference's double hue rounds to either side of the edge).
 template <bool kThr>
 __device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& e, const signed char* si8g,
-                                          const GridParams& gp, const FastCls& F, int& hN, int& hD) {
+                                          const GridParams& gp, const FastCls& F, int& hN, int& hD, int& gcol) {
     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb)), kd = kmx - kmn;
     const int si = si_of<kThr>(e, kmx, kd, si8g);
     // hue bin
@@ -131,12 +133,20 @@ __device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& 
     const int edge = (special ^ 1) & (int)(__mul24(hi, D) == N);
     const int vi = (e.vpack << 16) >> 16, gray = e.vpack >> 16;
     const int g = __mul24(__mul24(hi, gp.sp) + si, gp.vp) + vi;
+    gcol = g;
     // black (v < bt) > gray (s < gt) > edge > colour, as masks: a select chain
     // here is turned into a branch around the whole hue arithmetic
     const int mblack = -(int)(vi < 0);
     const int mgray = -(int)(si < 0) & ~mblack;
     const int medge = -edge & ~(mblack | mgray);
     return (g & ~(mblack | mgray | medge)) | ((gp.tl - 1) & mblack) | (gray & mgray) | (-2 & medge);
+}
+
+template <bool kThr>
+__device__ __forceinline__ int classify_e(int kr, int kg, int kb, const ClsEnt& e, const signed char* si8g,
+                                          const GridParams& gp, const FastCls& F, int& hN, int& hD) {
+    int gcol;
+    return classify_e<kThr>(kr, kg, kb, e, si8g, gp, F, hN, hD, gcol);
 }
 
 // The fused K1's classification: classify_e() on the half-bin grid (cells of

@@ -624,7 +624,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         max_slots = std::max(max_slots, h_ns[i]);
     }
     // the second pass on the tail stream, after K1, concurrent with the FFTs
-    const hipStream_t s2 = c->tail;
+    static const bool tail_on_fft = getenv("PHD_TAIL_ON_FFT") != nullptr;
+    const hipStream_t s2 = tail_on_fft ? (pipe ? sc : sf) : c->tail;
     PHD_HIP(hipStreamWaitEvent(s2, ev_k1, 0));
     uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
     const bool batched = ds <= 1 && (fused || palette_sums_b_lds(gp.tl, max_slots) <= 160 * 1024);
@@ -1237,15 +1238,21 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
     return 0;
 }
 
+constexpr long kMixedGroupMax = 1024;                         // images per run, any size
+
 // Image indices grouped by size (groups in order of first appearance, each in
-// index order), at most `cap` per group: one batched run per group.
-static std::vector<std::vector<int>> size_groups(const int* heights, const int* widths, int n, int cap) {
+// index order), at most `cap` per group, or (pix_cap > 0) as many as fit
+// pix_cap pixels when that is more: one batched run per group.
+static std::vector<std::vector<int>> size_groups(const int* heights, const int* widths, int n, int cap,
+                                                 long pix_cap = 0) {
     std::vector<std::vector<int>> g;
     std::map<std::pair<int, int>, int> open;                  // size -> its group still filling
     for (int i = 0; i < n; i++) {
         const auto key = std::make_pair(heights[i], widths[i]);
         auto it = open.find(key);
-        if (it == open.end() || (int)g[it->second].size() >= cap) {
+        const long npix = (long)heights[i] * widths[i];
+        const int c = std::max<long>(cap, std::min<long>(kMixedGroupMax, pix_cap / std::max(npix, 1L)));
+        if (it == open.end() || (int)g[it->second].size() >= c) {
             open[key] = (int)g.size();
             g.emplace_back();
         }
@@ -1266,7 +1273,10 @@ extern "C" int phd_report_batch_device_mixed(const uint8_t* const* d_images, con
     }
     Context* c = get_context();
     if (!c) return -1;
-    const auto groups = size_groups(heights, widths, n_images, 64);
+    // 64 images a run, or as many as 64 of the 12 MP headline size hold (small
+    // images: one run for a whole size instead of one per 64, so the per-run
+    // launches, host round trip and partly filled grids are paid a few times)
+    const auto groups = size_groups(heights, widths, n_images, 64, 64L * 12000000L);
     // the groups go to the lanes in order, each lane taking the next one when
     // it is done with its last
     std::atomic<size_t> next{0};

@@ -79,6 +79,8 @@ int main(int argc, char** argv) {
                d.parents.size(), d.search.size(),
                std::chrono::duration<double, std::micro>(t1 - t0).count() / iters);
     }
+    if (getenv("DUMP_RULES"))                           // partial groups: g keep dangle
+        for (int g : d.search) printf("rule %d %d %d\n", g, d.rules[g].keep, d.rules[g].dangle);
     if (!same(d, e)) {
         printf("MISMATCH on the saved histogram\n");
         return 1;

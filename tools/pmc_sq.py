@@ -1,6 +1,7 @@
 """SQ/LDS counter passes for one pipeline kernel (run ON the GPU box).
 
     python tools/pmc_sq.py KERNEL [--iters N]     (KERNEL: 0 hsv_stats, 1 fft_rows, 2 fft_cols)
+    python tools/pmc_sq.py 0 --probe 3000x4000:64   (tools/mixed_probe.py's full reports instead)
 
 Each pass is a separate `rocprofv3 --pmc ...` run (counters only, no trace
 domains) over tools/kbench.py; the per-kernel averages are printed and saved
@@ -23,21 +24,30 @@ PASSES = [
     ["SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64",
      "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS"],
 ]
-NAMES = ["k_k1t", "k_rgb_stats", "k_hsv_stats", "k_fft_rows", "k_fft_cols", "k_rows_ct", "k_cols_ct", "k_cutoffs", "k_palette_sums", "k_sharp"]
+NAMES = ["k_partial_sums", "k_k1t", "k_rgb_stats", "k_hsv_stats", "k_fft_rows", "k_fft_cols", "k_rows_ct", "k_cols_ct", "k_cutoffs", "k_palette_sums", "k_sharp"]
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("kernel", type=int)
     p.add_argument("--mask", default="0")
+    p.add_argument("--probe", default="", help="SHAPE:N -- profile tools/mixed_probe.py N at PROBE_SHAPES=SHAPE")
     a = p.parse_args()
+    target = [sys.executable, os.path.join(ROOT, "tools", "kbench.py"), str(a.kernel), a.mask]
+    env = dict(os.environ)
+    if a.probe:
+        shape, n = a.probe.split(":")
+        target = [sys.executable, os.path.join(ROOT, "tools", "mixed_probe.py"), n]
+        env["PROBE_SHAPES"] = shape
     res = {}
     for i, counters in enumerate(PASSES):
         out = os.path.join(ROOT, "gpurun_out", f"pmcsq_{a.kernel}_{i}")
-        cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", out, "-o", "p", "--",
-                                                  sys.executable, os.path.join(ROOT, "tools", "kbench.py"),
-                                                  str(a.kernel), a.mask]
-        r = subprocess.run(cmd, cwd=ROOT)
+        cmd = ["rocprofv3", "--pmc"] + counters + ["--output-format", "csv", "-d", out, "-o", "p", "--"] + target
+        try:
+            r = subprocess.run(cmd, cwd=ROOT, env=env, timeout=150)
+        except subprocess.TimeoutExpired:
+            print(f"pass {i} timed out")
+            break
         if r.returncode != 0:
             print(f"pass {i} failed rc={r.returncode}")
             continue
