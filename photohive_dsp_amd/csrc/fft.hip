@@ -235,9 +235,12 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     const int lds_bins = bins_bytes <= 48 * 1024;
     const size_t fixed = sizeof(double2) * (64 + plan.n_hi + kLogTab) + (lds_bins ? bins_bytes : 0);
     const size_t col_bytes = sizeof(double2) * height;
+    // columns per block: up to ~3k elements (several blocks per CU; measured
+    // on 64-image groups, per launch: 1080 rows C = 2 142 us against C = 8 196,
+    // 720 rows C = 4 130 against 171, 512 rows C = 4 54 against 69)
+    static const int cmax = getenv("PHD_FFT_COLS_C") ? atoi(getenv("PHD_FFT_COLS_C")) : 8;   // tuning
     int C = 1;
-    while (C < 8 && (size_t)(2 * C) * height <= (size_t)kFftMaxLds && (2 * C) * col_bytes + fixed <= kLdsBudget)
-        C *= 2;
+    while (C < cmax && (size_t)(2 * C) * height <= 3072 && (2 * C) * col_bytes + fixed <= kLdsBudget) C *= 2;
     if (lds_out) *lds_out = C * col_bytes + fixed;
     if (lds_bins_out) *lds_bins_out = lds_bins;
     return C;

@@ -549,6 +549,8 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                                   160 * 1024);
         (void)hipFuncSetAttribute((const void*)k_k1t<512, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_k1t<1024, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
         return true;
     }();
     (void)attr;
@@ -567,10 +569,23 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
         phd_launch((k_k1t<512, true>), dim3(grid), dim3(512), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs, k255,
                    out0, a_stride, h_stride, cshift2, g_ablate | env_ablate());
     } else {                                              // one 1024-thread block per CU
-        const size_t lds = (size_t)t_var(gp.tl, ncell, cshift, code_bytes<false>()).end;
         const int grid = (int)std::min<long>(nitems, (long)num_cus());
-        phd_launch((k_k1t<1024, false>), dim3(grid), dim3(1024), lds, st, d_imgs, npix, nchunks, nitems, gp, tabs,
-                   k255, out0, a_stride, h_stride, cshift, g_ablate | env_ablate());
+        // the triangular code table leaves 31 KiB more for lane copies of the
+        // cells (fine grids: 36/4/5's 3312 hue cells fit one copy beside the
+        // full table, two beside the triangle)
+        static const bool tri_off = getenv("PHD_K1_TRI1024") && atoi(getenv("PHD_K1_TRI1024")) == 0;
+        int cs_tri = -1;
+        for (int cs = 4; cs > cshift && !tri_off && cs_tri < 0; cs--)
+            if (t_var(gp.tl, ncell, cs, code_bytes<true>()).end <= 158 * 1024) cs_tri = cs;
+        if (cs_tri > cshift) {
+            const size_t lds = (size_t)t_var(gp.tl, ncell, cs_tri, code_bytes<true>()).end;
+            phd_launch((k_k1t<1024, true>), dim3(grid), dim3(1024), lds, st, d_imgs, npix, nchunks, nitems, gp,
+                       tabs, k255, out0, a_stride, h_stride, cs_tri, g_ablate | env_ablate());
+        } else {
+            const size_t lds = (size_t)t_var(gp.tl, ncell, cshift, code_bytes<false>()).end;
+            phd_launch((k_k1t<1024, false>), dim3(grid), dim3(1024), lds, st, d_imgs, npix, nchunks, nitems, gp,
+                       tabs, k255, out0, a_stride, h_stride, cshift, g_ablate | env_ablate());
+        }
     }
     return hipGetLastError();
 }

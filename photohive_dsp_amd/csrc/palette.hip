@@ -1068,12 +1068,20 @@ __global__ __launch_bounds__(kPartThreads) void k_partial_sums_img(
                     int hN, hD;
                     g[i] = classify_e<kThr>(kr, kg, kb, ent[max(kr, max(kg, kb))], si8, gp, fc, hN, hD, gc[i]);
                 }
+                // both candidates' entries read unconditionally (a select, not a
+                // branch per pixel that waits on its own LDS read): the group
+                // itself, or an edge pixel's colour groups gcol and one bin below
+                int ea[4], eb[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const bool c = g[i] >= 0 ? gent[g[i]] >= 0
-                                             : (gent[gc[i]] >= 0 || (gc[i] >= svp && gent[gc[i] - svp] >= 0));
-                    cand |= (unsigned)(c && p0 + i < end) << (4 * st + i);
+                    const int ga = g[i] >= 0 ? g[i] : gc[i];
+                    const int gb = (g[i] < 0 && gc[i] >= svp) ? gc[i] - svp : ga;
+                    ea[i] = gent[ga];
+                    eb[i] = gent[gb];
                 }
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    cand |= (unsigned)((ea[i] >= 0 || eb[i] >= 0) && p0 + i < end) << (4 * st + i);
             } else {
                 for (long p = p0; p < p0 + 4 && p < end && p < npix; p++) add(p, ip[3 * p], ip[3 * p + 1], ip[3 * p + 2]);
             }
