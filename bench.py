@@ -626,7 +626,7 @@ def config4(cx, total, h=3000, w=4000, iters=3):
                          "algorithmic_bytes_per_launch": ab, "avg_launch_us": round(us["fft_cols"], 2)}}
 
 
-def config5(cx, total, iters=2):
+def config5(cx, total, iters=4):
     """BASELINE config 5: `total` device-resident images of mixed sizes
     (shard.MIXED_SHAPES, 512^2 .. 6000x4000), full reports at h/s/v = 36/4/5,
     LPT-sharded by pixel count over the ranks (shard.assign), each rank one

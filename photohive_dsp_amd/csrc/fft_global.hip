@@ -51,7 +51,7 @@ __global__ __launch_bounds__(T) void k_gfft_direct(const double2* in, double2* o
     const double2* src = in + s0 * n;
     for (int i = tid; i < ns * n; i += T) buf[i] = src[i];
     __syncthreads();
-    fft_lds<T, GEN>(buf, ns, plan, tw, tw + 64);
+    fft_lds<T, GEN ? 2 : 0>(buf, ns, plan, tw, tw + 64);
     double2* dst = out + s0 * n;
     for (int i = tid; i < ns * n; i += T) dst[i] = buf[i];
 }
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(T) void k_gfft_4a(const double2* __restrict__ in, d
         buf[jj * n1 + j1] = jj < g ? x[(long)j1 * n2 + j20 + jj] : make_double2(0.0, 0.0);
     }
     __syncthreads();
-    fft_lds<T, GEN>(buf, G, p1, tw, tw + 64);
+    fft_lds<T, GEN ? 2 : 0>(buf, G, p1, tw, tw + 64);
     double2* y = scr + s * n;
     for (int i = tid; i < G * n1; i += T) {
         const int k1 = i / G, jj = i - k1 * G;
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(T) void k_gfft_4b(const double2* __restrict__ scr, 
     const double2* src = scr + s * n + (long)k10 * n2;
     for (int i = tid; i < G * n2; i += T) buf[i] = i < g * n2 ? src[i] : make_double2(0.0, 0.0);
     __syncthreads();
-    fft_lds<T, GEN>(buf, G, p2, tw, tw + 64);
+    fft_lds<T, GEN ? 2 : 0>(buf, G, p2, tw, tw + 64);
     double2* X = out + s * n;
     for (int i = tid; i < G * n2; i += T) {
         const int k2 = i / G, kk = i - k2 * G;

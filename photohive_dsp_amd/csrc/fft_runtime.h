@@ -7,6 +7,7 @@
 // accurate) and two small staged tables (e = 64*hi + lo).
 #pragma once
 
+#include "fft_engine.h"
 #include "phd_device.h"
 
 namespace phd {
@@ -88,6 +89,17 @@ __device__ __forceinline__ void butterfly<8>(double2 (&v)[8]) {
     }
 }
 
+// Composite radices (fewer LDS passes for the image lengths of config 5:
+// 1920 = 16 12 10, 1080 = 12 10 9): the compile-time engine's register
+// four-step DFTs (fft_engine.h, constant twiddles from fft_consts.h).
+template <int R>
+constexpr bool kComposite = R == 6 || R == 9 || R == 10 || R == 12 || R == 16;
+template <> __device__ __forceinline__ void butterfly<6>(double2 (&v)[6]) { fe::dft<6>(v); }
+template <> __device__ __forceinline__ void butterfly<9>(double2 (&v)[9]) { fe::dft<9>(v); }
+template <> __device__ __forceinline__ void butterfly<10>(double2 (&v)[10]) { fe::dft<10>(v); }
+template <> __device__ __forceinline__ void butterfly<12>(double2 (&v)[12]) { fe::dft<12>(v); }
+template <> __device__ __forceinline__ void butterfly<16>(double2 (&v)[16]) { fe::dft<16>(v); }
+
 // a / d for 0 <= a < 2^23 through one float multiply and an exact correction
 // (the float quotient is off by at most one at these magnitudes).
 __device__ __forceinline__ int fdiv(int a, int d, float inv) {
@@ -130,12 +142,16 @@ __device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns
             const int jh = fdiv(j, Ns, ins), jm = j - jh * Ns;
             if (jm != 0) {
                 const double2 w = twiddle(lo, hi, jm * tstep);
-                double2 wr = w;
-                v[b][1] = cmul(v[b][1], w);
+                if constexpr (kComposite<R>) {
+                    fe::twiddle_powers<R>(v[b], w);          // four interleaved power chains
+                } else {
+                    double2 wr = w;
+                    v[b][1] = cmul(v[b][1], w);
 #pragma unroll
-                for (int r = 2; r < R; r++) {
-                    wr = cmul(wr, w);
-                    v[b][r] = cmul(v[b][r], wr);
+                    for (int r = 2; r < R; r++) {
+                        wr = cmul(wr, w);
+                        v[b][r] = cmul(v[b][r], wr);
+                    }
                 }
             }
             butterfly<R>(v[b]);
@@ -189,7 +205,10 @@ __device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns,
     __syncthreads();
 }
 
-template <int T, bool GEN>
+// MODE bits over the radices 2, 3, 4, 5, 8: 1 the composites, 2 any other
+// radix (generic_pass).  A kernel instance holds only the passes its MODE
+// needs (a 16-point pass takes ~150 VGPRs, the small radices ~90).
+template <int T, int MODE>
 __device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan, const double2* lo, const double2* hi) {
     int Ns = 1;
     for (int p = 0; p < plan.npass; p++) {
@@ -201,7 +220,14 @@ __device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan, const doubl
             case 5: stockham_pass<5, T>(buf, plan.n, nseq, Ns, lo, hi); break;
             case 8: stockham_pass<8, T>(buf, plan.n, nseq, Ns, lo, hi); break;
             default:
-                if constexpr (GEN) generic_pass<T>(buf, plan.n, nseq, Ns, R, plan.tw);
+                if constexpr ((MODE & 1) != 0) {
+                    if (R == 6) { stockham_pass<6, T>(buf, plan.n, nseq, Ns, lo, hi); break; }
+                    if (R == 9) { stockham_pass<9, T>(buf, plan.n, nseq, Ns, lo, hi); break; }
+                    if (R == 10) { stockham_pass<10, T>(buf, plan.n, nseq, Ns, lo, hi); break; }
+                    if (R == 12) { stockham_pass<12, T>(buf, plan.n, nseq, Ns, lo, hi); break; }
+                    if (R == 16) { stockham_pass<16, T>(buf, plan.n, nseq, Ns, lo, hi); break; }
+                }
+                if constexpr ((MODE & 2) != 0) generic_pass<T>(buf, plan.n, nseq, Ns, R, plan.tw);
                 break;
         }
         Ns *= R;

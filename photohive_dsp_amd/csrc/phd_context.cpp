@@ -218,7 +218,7 @@ bool ensure_pinned(Context* c, size_t need) {
 }
 
 // ---- FFT plans ---------------------------------------------------------------
-bool make_fft_plan(int n, FftPlanHost* p) {
+bool make_fft_plan(int n, FftPlanHost* p, bool composite) {
     if (n < 1 || n > kFftMaxLds) {
         set_error("FFT length " + std::to_string(n) + " exceeds the LDS-resident limit " +
                   std::to_string(kFftMaxLds) + " of this build");
@@ -228,6 +228,13 @@ bool make_fft_plan(int n, FftPlanHost* p) {
     P.n = n;
     P.npass = 0;
     int m = n;
+    static const bool small_radices = getenv("PHD_FFT_SMALL_RADICES") != nullptr;   // A/B only
+    if (composite && n <= 4096 && !small_radices) {
+        // largest radix first: fewer LDS passes (1920 = 16 12 10 in three
+        // instead of 8 8 5 3 2 in five)
+        for (int r : {16, 12, 10, 9, 8, 6, 5, 4, 3, 2})
+            while (m % r == 0 && P.npass < kMaxFftPasses) { P.radix[P.npass++] = r; m /= r; }
+    }
     // radix order: 8s, then 4, then 2, 5, 3, then any remaining prime factor
     while (m % 8 == 0 && P.npass < kMaxFftPasses) { P.radix[P.npass++] = 8; m /= 8; }
     if (m % 4 == 0) { P.radix[P.npass++] = 4; m /= 4; }
@@ -244,9 +251,12 @@ bool make_fft_plan(int n, FftPlanHost* p) {
         return false;
     }
     P.generic = 0;
+    P.composite = 0;
     for (int i = 0; i < P.npass; i++) {
         const int r = P.radix[i];
-        if (r != 2 && r != 3 && r != 4 && r != 5 && r != 8) P.generic = 1;
+        const bool comp = r == 6 || r == 9 || r == 10 || r == 12 || r == 16;
+        if (r != 2 && r != 3 && r != 4 && r != 5 && r != 8 && !comp) P.generic = 1;
+        P.composite |= comp ? 1 : 0;
     }
     P.n_hi = (n + 63) / 64;
     const long double two_pi = 6.283185307179586476925286766559005768L;
@@ -269,12 +279,13 @@ bool make_fft_plan(int n, FftPlanHost* p) {
     return true;
 }
 
-const FftPlanHost* get_plan(Context* c, int n) {
-    auto it = c->plans.find(n);
+const FftPlanHost* get_plan(Context* c, int n, bool composite) {
+    const auto key = std::make_pair(n, composite);
+    auto it = c->plans.find(key);
     if (it != c->plans.end()) return &it->second;
     FftPlanHost p;
-    if (!make_fft_plan(n, &p)) return nullptr;
-    return &(c->plans[n] = p);
+    if (!make_fft_plan(n, &p, composite)) return nullptr;
+    return &(c->plans[key] = p);
 }
 
 const double2* get_ct_twiddles(Context* c, int n, bool rows) {
@@ -374,7 +385,10 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         return true;
     }
     if (!gfft_direct_ok(width) || !gfft_direct_ok(height)) return select_generic(c, height, width, nbins, s);
-    s->prow = get_plan(c, width);
+    // composite radices for the row pass only: measured on 64-image groups
+    // (per launch) rows of 1280 130 against 213 us, of 640 97 against 136;
+    // the column pass ran slower with them (1080-row columns 176 against 146)
+    s->prow = get_plan(c, width, true);
     s->pcol = get_plan(c, height);
     if (!s->prow || !s->pcol) return false;
     const int wf = width / 2 + 1;

@@ -93,7 +93,9 @@ struct FftPlanHost {
     FftPlan plan{};
     double2* d_tw = nullptr;
 };
-bool make_fft_plan(int n, FftPlanHost* p);
+// composite: radices up to 16 (the image passes' kernels, fft.hip); else 2, 3,
+// 4, 5, 8 and generic (fft_global.hip, which runs them at up to 1024 threads)
+bool make_fft_plan(int n, FftPlanHost* p, bool composite = false);
 
 // A batched 1-D transform of length n over sequences in HBM (fft_global.hip):
 // one LDS pass (direct), two (four-step n = n1 * n2) or Bluestein's
@@ -160,7 +162,7 @@ struct Context {
     int device = -1;
     hipStream_t stream = nullptr;
     double* d_k255 = nullptr;                       // k/255.0 for k in [0,256)
-    std::map<int, FftPlanHost> plans;
+    std::map<std::pair<int, bool>, FftPlanHost> plans;   // (length, composite)
     std::map<std::pair<int, int>, double2*> ct_tw;  // (length, rows?) -> compile-time plan twiddles
     std::map<std::tuple<int, int, int, int>, BlurTable> tables;
     std::map<std::tuple<int, int, int, int, int>, ColWin> colwins;   // (H, W, nr, na, grid)
@@ -267,7 +269,7 @@ int lanes_setting();
 hipStream_t work_stream(Context* c, void* stream);
 bool ensure_device(void** p, size_t* cap, size_t need);
 bool ensure_pinned(Context* c, size_t need);
-const FftPlanHost* get_plan(Context* c, int n);
+const FftPlanHost* get_plan(Context* c, int n, bool composite = false);
 // Per-pass twiddle tables of the compile-time plan of length n (rows or columns).
 const double2* get_ct_twiddles(Context* c, int n, bool rows);
 

@@ -129,7 +129,8 @@ struct GroupRule {
 struct FftPlan {
     int n;
     int npass;
-    int generic;               // some radix is outside {2,3,4,5,8}
+    int generic;               // some radix is outside {2,3,4,5,6,8,9,10,12,16}
+    int composite;             // some radix is 6, 9, 10, 12 or 16 (image-pass plans only)
     int n_hi;                  // entries of tw_hi = ceil(n / 64)
     int radix[kMaxFftPasses];
     const double2* tw;         // device: tw[t] = W_n^t, t in [0, n)
