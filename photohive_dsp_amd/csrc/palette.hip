@@ -1659,8 +1659,8 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     if (!per_group && max_per_image <= kPartImgMax && max_per_image > 1) {
         const size_t lds = PartImgLds::bytes(gp.tl);
         // (grid.y 16: same step time; 4: 4 % slower, the walks then outlast the FFTs they share the CUs with)
-        static const int gy = getenv("PHD_PART_GY") ? std::max(1, atoi(getenv("PHD_PART_GY"))) : 64;
-        const dim3 grid(n, gy);
+        // (grid.y 256 measured the same as 64 in config 5, round 3)
+        const dim3 grid(n, 64);
 #define PHD_PI_LAUNCH(A, T)                                                                                     \
     phd_launch((k_partial_sums_img<A, T>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc, tabs, \
                        k255, entries, n_entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride)
