@@ -169,8 +169,10 @@ int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int height, int wi
                           const phd_config* cfg, double* bins_out, Blur_Vector* vectors_out, void* stream);
 
 /* Device-resident images of any sizes (config 5 of BASELINE.json): one
- * batched run per group of same-size images.  Returns 0 when every image
- * succeeded, else the number of failures, or -1 on a setup error. */
+ * batched run per group of same-size images (64 images, or as many as hold
+ * 64 x 12 MP when that is more: up to 1024 small images in one run).  Returns
+ * 0 when every image succeeded, else the number of failures, or -1 on a setup
+ * error. */
 int phd_report_batch_device_mixed(const uint8_t* const* d_images, const int* heights, const int* widths,
                                   int n_images, const phd_config* cfg, Full_Report_Data** out, int* status,
                                   void* stream);

@@ -57,3 +57,25 @@ def test_column_bin_windows_bit_identical(shape):
         L.lib.phd_debug_col_windows(prev)
     assert np.array_equal(on_bins, off_bins)
     assert on_vecs == off_vecs
+
+
+def test_mixed_batch_groups_past_64_images():
+    """phd_report_batch_device_mixed runs small sizes in groups larger than 64
+    (pixel budget, phd_report.cpp size_groups): 70 images of 352x352 between
+    three of 400x400, every report equal to its single-image device report."""
+    L, torch = _lib()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import report_device, reports_device_mixed
+    shapes = [(352, 352)] * 35 + [(400, 400)] * 3 + [(352, 352)] * 35
+    imgs = [torch.from_numpy(synth.make(("structured", "uniform", "dominant")[i % 3], h, w, 300 + i)).cuda()
+            for i, (h, w) in enumerate(shapes)]
+    kw = dict(h_partitions=36, s_partitions=4, v_partitions=5)
+    reps = reports_device_mixed(imgs, **kw)
+    for i in list(range(0, len(imgs), 7)) + [35, 36, 37, len(imgs) - 1]:
+        one = report_device(imgs[i][None].contiguous(), **kw)[0]
+        r = reps[i]
+        assert r.color_palette.group_ids == one.color_palette.group_ids
+        assert r.color_palette.quantities == one.color_palette.quantities
+        np.testing.assert_allclose(np.array(r.color_palette.hsv), np.array(one.color_palette.hsv), rtol=1e-12)
+        assert np.array_equal(np.array(r.blur_profile.bins), np.array(one.blur_profile.bins))
+        assert r.blur_vectors == one.blur_vectors
