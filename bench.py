@@ -811,6 +811,10 @@ def main(argv=None):
                     traffic = pm["kernels"][dom]["hbm_bytes_per_image"] * per_launch
                     tsrc = (f"{os.path.relpath(args.pmc, ROOT)}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                             "passes of this config (tools/pmc_collect.py), not measured in this run")
+                    if pm.get("calibration"):
+                        f = pm["kernels"][dom].get("fetch_factor")
+                        tsrc += (f"; FETCH_SIZE x {f:.3f} for this kernel's access pattern, calibrated on its "
+                                 f"algorithmic bytes ({pm['calibration']})")
             except (OSError, ValueError, KeyError):
                 pass
             line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),

@@ -65,15 +65,32 @@ def main():
     images = ba.batch * (ba.steps + max(1, ba.warmup))     # every step, warmup included, is profiled
     res = {"image": f"{a.height}x{a.width}", "source": [os.path.relpath(f1, ROOT), os.path.relpath(f2, ROOT)],
            "bench_args": bench_args,
-           "correction": "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halving)",
+           "correction": "hbm_bytes = fetch_factor*FETCH_SIZE*1024 + WRITE_SIZE*1024 (fetch_factor 2 for streaming "
+                         "reads, MI355X_MICROARCH.md; calibrated per FFT pass where profiles/pmc_calib.json has it)",
            "kernels": {}}
+    # FETCH_SIZE -> bytes: x2 for 16-B-per-lane streaming reads (the guide's
+    # calibration); the FFT passes' own patterns are calibrated on their
+    # algorithmic bytes by tools/pmc_calib.py (profiles/pmc_calib.json)
+    factors = {}
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_calib.json")) as f:
+            cal = json.load(f)
+        for kname, short_name in (("k_cols_ct", "fft_cols"), ("k_rows_ct", "fft_rows")):
+            if kname in cal and cal.get("image") == f"{a.height}x{a.width}":
+                factors[short_name] = cal[kname]["factor"]
+        if factors:
+            res["calibration"] = "profiles/pmc_calib.json (tools/pmc_calib.py)"
+    except (OSError, ValueError, KeyError):
+        pass
     for k in sorted(set(fetch) | set(write)):
         (fk, n), (wk, _) = fetch.get(k, (0.0, 0)), write.get(k, (0.0, 0))
         per_launch = images / max(n, 1)
-        hbm = 2 * fk * 1024 + wk * 1024
-        res["kernels"][k] = {"fetch_size_kb": fk, "write_size_kb": wk, "launches": n,
+        fac = factors.get(k, 2.0)
+        hbm = fac * fk * 1024 + wk * 1024
+        res["kernels"][k] = {"fetch_size_kb": fk, "write_size_kb": wk, "launches": n, "fetch_factor": fac,
                              "images_per_launch": per_launch, "hbm_bytes_per_launch": hbm,
-                             "hbm_bytes_per_image": hbm / per_launch}
+                             "hbm_bytes_per_image": hbm / per_launch,
+                             "hbm_bytes_per_launch_x2": 2 * fk * 1024 + wk * 1024}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     # profiles/ for bench.py on this box; gpurun_out/ is what travels back
     for d, name in ((os.path.join(ROOT, "profiles"), "pmc_latest.json"),
