@@ -123,32 +123,75 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
         for (int i = tid; i < nc * H; i += T) buf[i] = src[i];
     }
     __syncthreads();
-    if (!(ablate & 1)) fft_lds<T, MODE>(buf, nc, plan, tw, tw + 64);
-    double mx = 0.0;
-    unsigned long long* acc = lds_bins ? lb : bin_sums;
+    // this thread's contiguous run of elements and their bin ids, loaded
+    // before the FFT so the loads are in flight during it (element i of the
+    // block is row i % H of column k0 + i / H; the nc columns' bin ids are
+    // one contiguous run of the map)
+    constexpr int kPer = 8;                               // elements per thread (nc * H <= 8 T)
     const int total = (ablate & 2) ? 0 : nc * H;
-    for (int i0 = 0; i0 < total; i0 += T) {
-        const int i = i0 + tid;
-        int b = -1;
-        unsigned long long lg = 0ull;
+    const int per = (total + T - 1) / T, i0 = tid * per, i1 = min(total, i0 + per);
+    int bv[kPer];
+    {
+        const uint16_t* bmap = binmap + (size_t)k0 * H;
+#pragma unroll
+        for (int j = 0; j < kPer; j++) bv[j] = i0 + j < i1 ? (int)bmap[i0 + j] : -1;
+    }
+    if (!(ablate & 1)) fft_lds<T, MODE>(buf, nc, plan, tw, tw + 64);
+    // p = |X|^2 per element (1 for p < 1, whose log the reference clamps
+    // away), written over the spectrum as doubles: read to registers first
+    double mx = 0.0;
+    double pv[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        const int i = tid + j * T;
+        pv[j] = 1.0;
         if (i < total) {
             const double2 X = buf[i];
-            const double p = X.x * X.x + X.y * X.y;      // fft_processing.c:49
+            const double p = X.x * X.x + X.y * X.y;          // fft_processing.c:49
             mx = fmax(mx, p);
-            if (p >= 1) {                               // fft_processing.c:197-198
-                const int c = i / H, u = i - c * H;
-                b = binmap[(size_t)(k0 + c) * H + u];
-                lg = bin_fixed(log_mant(p, lt), bscale);
+            pv[j] = p >= 1 ? p : 1.0;                        // fft_processing.c:197-198
+        }
+    }
+    __syncthreads();
+    double* lgb = reinterpret_cast<double*>(buf);
+#pragma unroll
+    for (int j = 0; j < kPer; j++)
+        if (tid + j * T < total) lgb[tid + j * T] = pv[j];
+    __syncthreads();
+    // runs of one polar bin summed as the log of their product (frexp
+    // mantissas multiply, exponents add, one fp64 log per run), one atomic per
+    // run; the thread's first two runs are logged after the unrolled walk (as
+    // fft_ct.hip's walk_runs)
+    unsigned long long* acc = lds_bins ? lb : bin_sums;
+    {
+        auto flush = [&](int b, double m, int e) {
+            const double a = fmax((double)e * 0.69314718055994530942 + log_mant(m, lt), 0.0);
+            if (a > 0.0) atomicAdd(&acc[b], bin_fixed(a, bscale));
+        };
+        int cur = -1, esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
+        double mprod = 1.0, m0 = 1.0, m1 = 1.0;
+        auto close = [&]() {
+            if (n == 0) { b0 = cur; m0 = mprod; e0 = esum; n = 1; }
+            else if (n == 1) { b1 = cur; m1 = mprod; e1 = esum; n = 2; }
+            else flush(cur, mprod, esum);
+        };
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+            if (bv[j] >= 0) {
+                if (bv[j] != cur) {
+                    if (cur >= 0) close();
+                    cur = bv[j];
+                    mprod = 1.0;
+                    esum = 0;
+                }
+                int e;
+                mprod *= frexp(lgb[i0 + j], &e);
+                esum += e;
             }
         }
-        // fixed-point integers: the sums do not depend on the atomics' order
-        const int b0 = __builtin_amdgcn_readfirstlane(b);
-        if (__all(b == b0)) {
-            const unsigned long long t = wave_sum(lg);
-            if (b0 >= 0 && lane_id() == 0) atomicAdd(&acc[b0], t);
-        } else if (b >= 0) {
-            atomicAdd(&acc[b], lg);
-        }
+        if (cur >= 0) close();
+        if (n > 0) flush(b0, m0, e0);
+        if (n > 1) flush(b1, m1, e1);
     }
     // block max -> one partial per block (a per-wave atomicMax on one word
     // serialised ~16K atomics per image: ~160 us, DESIGN.md ablation)
