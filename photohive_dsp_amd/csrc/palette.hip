@@ -1659,8 +1659,10 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     if (!per_group && max_per_image <= kPartImgMax && max_per_image > 1) {
         const size_t lds = PartImgLds::bytes(gp.tl);
         // (grid.y 16: same step time; 4: 4 % slower, the walks then outlast the FFTs they share the CUs with)
-        // (grid.y 256 measured the same as 64 in config 5, round 3)
-        const dim3 grid(n, 64);
+        // split each image's walk over ~4096 blocks in all, at least 64 per
+        // image (grid.y 256 measured the same as 64 in config 5's 64-image
+        // groups; a single image's walk over 64 blocks outlasts its FFTs)
+        const dim3 grid(n, std::max(64, std::min(1024, 4096 / std::max(n, 1))));
 #define PHD_PI_LAUNCH(A, T)                                                                                     \
     phd_launch((k_partial_sums_img<A, T>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc, tabs, \
                        k255, entries, n_entries, chunk_hist0, h_stride, rules0, off0, b_stride, out0, c_stride)
@@ -1675,7 +1677,9 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
         return hipGetLastError();
     }
     const size_t lds = K1Lds::qn;
-    const dim3 grid(n_entries, 32);
+    // ~4096 blocks in all, at least 32 per entry (a single entry's walk over 32
+    // blocks took 61 us at 4000x3000, past the image's FFTs)
+    const dim3 grid(n_entries, std::max(32, std::min(1024, 4096 / std::max(n_entries, 1))));
     if (fc.use_thr) {
         if (aligned)
             phd_launch((k_partial_sums_b<true, true>), grid, dim3(kPartThreads), lds, st, d_imgs, npix, gp, fc,
