@@ -41,9 +41,10 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=4)
-    p.add_argument("--batch", type=int, default=64,
-                   help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64; "
-                        "the per-call fixed costs amortised, profiles/r02/batch_lanes.md)")
+    p.add_argument("--batch", type=int, default=256,
+                   help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64, "
+                        "7.0-7.3k at 128, 7.4k at 256 on one box (round 3): the per-call fixed costs -- K1's "
+                        "prologue and tail, the host head and tail of a call -- amortised; 9.2 GB of pixels)")
     p.add_argument("--lanes", type=int, default=1,
                    help="library lanes for every config of the run (phd_set_lanes; the library's default is 1): "
                         "1 keeps each kernel launch alone on the GPU, so its event duration prices the kernel "

@@ -13,7 +13,8 @@ import bench  # noqa: E402
 
 def main():
     legs = sys.argv[1:] or ["config3"]
-    args = bench.parse(["--steps", os.environ.get("ONLY_STEPS", "30"), "--warmup", "4"])
+    args = bench.parse(["--steps", os.environ.get("ONLY_STEPS", "30"), "--warmup", "4",
+                        "--batch", os.environ.get("ONLY_BATCH", "64")])
     import torch
     torch.cuda.set_device(0)
     import photohive_dsp_amd  # noqa: F401
