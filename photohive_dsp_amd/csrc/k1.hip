@@ -400,7 +400,9 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         // deferred pixels (a hue exactly on a half-bin boundary, ~1.7 % of uniform
         // pixels): the thread counts its own in fp64 from the chunk words it still
         // holds (no LDS queue, no extra barrier; measured the same time as the
-        // queue resolved by the whole block, and as a 4 MiB decision table)
+        // queue resolved by the whole block, and as a 4 MiB decision table; a
+        // per-wave queue filled by a lane scan, round 3, 2.55 against 2.51 ms per
+        // 64-image launch: its extra registers doubled the VGPR spills)
         while (emask) {
             const int bt = __ffs(emask) - 1;
             emask &= emask - 1;
