@@ -181,6 +181,8 @@ struct Context {
     };
     std::map<std::tuple<int, int, int, double, double>, Cls> cls;
     // grow-only workspaces
+    std::vector<PaletteDecision> dec_scratch;       // run_reports' per-image decisions
+    std::vector<std::vector<double>> hsum_scratch;  // and host slot sums
     void* d_ws = nullptr;
     size_t ws_bytes = 0;
     void* h_pin = nullptr;
