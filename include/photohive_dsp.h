@@ -103,8 +103,11 @@ Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundaries* salien
                                        float saturation_value_weight, double fft_streak_thresh,
                                        double magnitude_thresh, int blur_cutoff_ratio_denom);
 
-/* Replaces free_full_report, src/interface.c:97-111: frees the whole tree and
- * sets *report = NULL. */
+/* Replaces free_full_report, src/interface.c:97-111: releases the whole tree
+ * and sets *report = NULL.  A report of this library is one heap block (every
+ * structure and array of the tree inside it), recycled for later reports of
+ * the same size; release it only through this call (as the reference's
+ * callers do), never by free() on its members. */
 void free_full_report(Full_Report_Data** report);
 /* free_full_report over an array of n reports (a batch call's `out`); NULL entries are skipped. */
 void phd_free_reports(Full_Report_Data** reports, int n);
