@@ -34,6 +34,9 @@ int newton_int_sqrt(double val) {       // src/utilities.c:43-52
 
 }  // namespace
 
+// T <= 1024 threads: at most 2046 bytes of run plus a 16-byte load
+constexpr size_t kBinMapPad = 4096;
+
 bool build_blur_table(int height, int width, int nr, int na, BlurTable* t) {
     const int wf = width / 2 + 1;
     t->height = height;
@@ -95,9 +98,10 @@ bool build_blur_table(int height, int width, int nr, int na, BlurTable* t) {
     t->counts.assign((size_t)na * nr, 0);
     for (unsigned i = 0; i < nth; i++)
         for (size_t b = 0; b < t->counts.size(); b++) t->counts[b] += part[i][b];
-    // + 64 bytes: the FFT column kernel loads each thread's run of bin ids with
-    // 16-byte loads that may read past the last column's end
-    if (hipMalloc(&t->d_map, map.size() * sizeof(uint16_t) + 64) != hipSuccess) {
+    // + kBinMapPad bytes: the FFT column kernels load each thread's run of bin
+    // ids (T threads x ceil(H / T) rows, up to T - 1 rows and a 16-byte load
+    // past the last column's end)
+    if (hipMalloc(&t->d_map, map.size() * sizeof(uint16_t) + kBinMapPad) != hipSuccess) {
         set_error("hipMalloc of the blur bin table failed");
         return false;
     }
@@ -143,8 +147,8 @@ bool build_col_windows(const BlurTable& t, int grid, const std::vector<int>& own
             lc[u] = (uint16_t)((pb - a0[b]) * win[2 * b + 1] + (rb - r0[b]));
         }
     }
-    // + 64 bytes as d_map (16-byte loads past the last column's end)
-    if (hipMalloc(&w->d_lmap, lmap.size() * sizeof(uint16_t) + 64) != hipSuccess ||
+    // + kBinMapPad bytes as d_map (runs past the last column's end)
+    if (hipMalloc(&w->d_lmap, lmap.size() * sizeof(uint16_t) + kBinMapPad) != hipSuccess ||
         hipMalloc(&w->d_win, win.size() * sizeof(int)) != hipSuccess ||
         hipMemcpy(w->d_lmap, lmap.data(), lmap.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(w->d_win, win.data(), win.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {

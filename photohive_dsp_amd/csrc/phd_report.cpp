@@ -189,8 +189,22 @@ struct ReportPool {
     }
 };
 ReportPool& report_pool() {
-    static ReportPool* p = new ReportPool;   // process lifetime (reports may be freed at exit)
-    return *p;
+    // process lifetime (reports may be freed at exit); a forked child starts
+    // a pool of its own (the parent's mutex may have been held at the fork)
+    static std::atomic<ReportPool*> p{nullptr};
+    static std::atomic<pid_t> owner{0};
+    ReportPool* q = p.load();
+    if (!q || owner.load() != getpid()) {
+        static std::mutex init;
+        std::lock_guard<std::mutex> lk(init);
+        q = p.load();
+        if (!q || owner.load() != getpid()) {
+            q = new ReportPool;
+            p.store(q);
+            owner.store(getpid());
+        }
+    }
+    return *q;
 }
 size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
