@@ -153,7 +153,8 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
                                                const unsigned long long* __restrict__ sums,
                                                const double* __restrict__ k255g, const double2* __restrict__ twg,
                                                double2* __restrict__ inter, int ablate_arg,
-                                               unsigned long long* __restrict__ rsum) {
+                                               unsigned long long* __restrict__ rsum,
+                                               const uint8_t* const* __restrict__ imgs, int nimg, long istride) {
     using K = RowK<W, T, Rs...>;
     const int ablate = PHD_ABL(ablate_arg);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -162,20 +163,28 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     const int tid = threadIdx.x;
     for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
     // schedule: line group m (pairs 4m..4m+3) on XCD m % 8, its 4 pairs on 4
-    // blocks of that XCD (gridDim.x is a multiple of 32)
-    const int P = (H + 1) / 2;
+    // blocks of that XCD (gridDim.x is a multiple of 32).  A batch (imgs, nimg
+    // images whose P is a multiple of 4, intermediates istride apart) numbers
+    // its images' line groups one after the other.
+    const int P = (H + 1) / 2, G = (P + 3) / 4;
     const int x = blockIdx.x & 7, q = blockIdx.x >> 3, QA = gridDim.x >> 5;
     const int a = q >> 2, i4 = q & 3;
-    auto pair_of = [&](int s) { return 4 * (x + 8 * (a + s * QA)) + i4; };
+    // step s's image and row pair (false past the last)
+    auto item = [&](int s, int& im, int& pr) {
+        const int m = x + 8 * (a + s * QA);
+        im = m / G;
+        pr = 4 * (m - im * G) + i4;
+        return im < nimg && pr < P;
+    };
 
     // the next pair's pixels, loaded straight into the registers the luma code
     // reads (no moves, so nothing waits for the loads before they are used);
     // groups past the row end re-load group 0 (unused, no branch)
     u32x3a rg[K::LR][2];
-    auto fetch = [&](int pr) {
+    auto fetch = [&](int im, int pr) {
         // (byte addressing: a 3-vector's sizeof is 16, a group is 12 bytes)
         const int y0 = 2 * pr;
-        const uint8_t* r0 = img + (size_t)y0 * 3 * W;
+        const uint8_t* r0 = (imgs ? imgs[im] : img) + (size_t)y0 * 3 * W;
         const uint8_t* r1 = (y0 + 1 < H) ? r0 + 3 * W : r0;
 #pragma unroll
         for (int j = 0; j < K::LR; j++) {
@@ -184,8 +193,9 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
             rg[j][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x3a*>(r1 + 12 * g));
         }
     };
-    int s = 0, pr = pair_of(0);
-    if (pr < P) fetch(pr);
+    int s = 0, im = 0, pr = 0;
+    bool live = item(0, im, pr);
+    if (live) fetch(im, pr);
     __syncthreads();
     unsigned cs[3] = {0u, 0u, 0u};    // this thread's channel sums (u32: a few row pairs of bytes)
     const int rot = (tid >> 1) & 3;   // b128 write swizzle: 8 lanes of a group hit 8 distinct 16-B slots
@@ -235,8 +245,9 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
         }
         // unconditional (past the last pair it re-reads this one): every path into
         // the loop head then has the same memory operations in flight
-        const int prn = pair_of(s + 1);
-        if (!(ablate & 4)) fetch(prn < P ? prn : pr);
+        int imn, prn;
+        const bool next = item(s + 1, imn, prn);
+        if (!(ablate & 4)) fetch(next ? imn : im, next ? prn : pr);
         __syncthreads();
         if (!(ablate & 1)) fft_lds<W, T, 1, Rs...>(buf, tw, tid);
         constexpr int WF = W / 2 + 1, KP = (WF + 1) / 2;
@@ -244,7 +255,7 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
         // k = 2(i/4) + (i/2)%2, row y0 + i%2); the phantom column WF (odd WF) is 0
         // (a fixed, unrolled count per thread, branch-free: the next step's wait
         // for its prefetched pixels can then count these stores exactly)
-        double2* orow = inter + (size_t)pr * KP * 4;
+        double2* orow = inter + im * istride + (size_t)pr * KP * 4;
         constexpr int NSO = (4 * KP + T - 1) / T;
 #pragma unroll
         for (int j = 0; j < NSO; j++) {
@@ -265,9 +276,11 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
         }
         __syncthreads();
         s++;
+        im = imn;
         pr = prn;
+        live = next;
     };
-    while (pr < P) step();
+    while (live) step();
     if (rsum) {
         // block sums through LDS (free after the last step's barrier), one atomic per channel
         unsigned long long* red = reinterpret_cast<unsigned long long*>(smem);
@@ -326,13 +339,14 @@ struct ColK {
 // each line is fetched once into that XCD's L2 (the grid is a multiple of 32).
 // one-column blocks are sized for two resident blocks per CU
 template <int H, int T, int CPB, int... Rs>
-__global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter, int wf,
+__global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
                                                      const uint16_t* __restrict__ binmap, int nbins,
                                                      const int* __restrict__ win, int nr,
-                                                     unsigned long long* __restrict__ bin_sums, double* __restrict__ fmax_part,
+                                                     unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
                                                      const double2* __restrict__ twg,
-                                                     const unsigned long long* __restrict__ sums, int width,
-                                                     double* __restrict__ dbg, double bscale, int ablate_arg) {
+                                                     const unsigned long long* __restrict__ sums0, int width,
+                                                     double* __restrict__ dbg, double bscale, int ablate_arg,
+                                                     int nimg, long istride, long bstride, long fstride, long sstride) {
     using K = ColK<H, T, CPB, Rs...>;
     constexpr int NC = K::NC;
     const int ablate = PHD_ABL(ablate_arg);
@@ -344,6 +358,13 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     double2* lt = tw + K::NTW;                                 // log_mant's table
     unsigned long long* lb = reinterpret_cast<unsigned long long*>(lt + kLogTab);
     const int tid = threadIdx.x;
+    // a batch: nimg images of one size, their intermediates, bin sums, max
+    // partials and channel sums istride / bstride / fstride / sstride apart;
+    // each block runs its columns of every image in turn
+    const double2* inter = inter0;
+    unsigned long long* bin_sums = bin_sums0;
+    double* fmax_part = fmax_part0;
+    const unsigned long long* sums = sums0;
     // NC == 1: blocks b, b^8, b^16, b^24 (one XCD) take the four columns of a
     // 128-byte line (two tiles), so each line is fetched once into that L2
     // NC == 2: blocks b, b^8 (one XCD) take the two tiles of a 128-byte line
@@ -355,13 +376,16 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     if (!K::GB)
         for (int i = tid; i < nbins; i += NT) lb[i] = 0ull;
     log_table_init(lt, tid, NT);
-    unsigned long long* const bsum = K::GB ? bin_sums : lb;   // where the runs are added
+    unsigned long long* bsum = K::GB ? bin_sums : lb;         // where the runs are added
     const int kpn = (wf + 1) / 2;
     const int nunit = (kpn + 1) / 2;                          // tile pairs (128-byte lines)
     const int nlog = NC == 2 ? (int)gridDim.x / 2 : (int)gridDim.x / 4;
     const int lblk = NC == 2 ? (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7))
                              : (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
-    const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
+    // a batch numbers its images' units one after the other: a block's range
+    // may span the end of one image and the start of the next (small images)
+    const long nall = (long)nimg * nunit;
+    const int c0 = (int)(lblk * nall / nlog), c1 = (int)((lblk + 1) * nall / nlog);
     // the column pair of step u (NC == 1: tile 2u or 2u+1; past the last tile
     // the block re-reads the last one and idles)
     auto pair_at = [&](int u) { return min(2 * u + (quad >> 1), kpn - 1); };
@@ -396,11 +420,22 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
             }
         }
     };
-    if (K::P0R && c0 < c1) fetch0(pair_at(c0));
-    else if (K::PF && c0 < c1) PHD_COL_FETCH(pair_at(c0));
+    // (a block without units still runs one empty segment: its max partial and
+    // bins are written as the one-image form always did)
+    for (int seg = c0, im = c0 / nunit, first = 1; first || seg < c1; im++, first = 0) {
+    // this image's units in the block's range: [u0, un) of image im
+    const int u0 = seg - im * nunit, un = min(c1 - im * nunit, nunit);
+    seg = im * nunit + un;
+    inter = inter0 + im * istride;
+    bin_sums = bin_sums0 + im * bstride;
+    fmax_part = fmax_part0 + im * fstride;
+    sums = sums0 + im * sstride;
+    if (K::GB) bsum = bin_sums;
+    if (K::P0R && u0 < un) fetch0(pair_at(u0));
+    else if (K::PF && u0 < un) PHD_COL_FETCH(pair_at(u0));
     double mx = 0.0;
     __syncthreads();
-    for (int u = c0; u < c1; u++) {
+    for (int u = u0; u < un; u++) {
         const int kp = pair_at(u);
         if (!K::PF) PHD_COL_FETCH(kp);
         if constexpr (K::P0R) {
@@ -444,7 +479,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                     bmw[j] = (unsigned)bcol[2 * j] | ((unsigned)bcol[2 * j + 1] << 16);
             }
         }
-        if (!K::P0R && K::PF && u + 1 < c1 && !(ablate & 4)) PHD_COL_FETCH(pair_at(u + 1));
+        if (!K::P0R && K::PF && u + 1 < un && !(ablate & 4)) PHD_COL_FETCH(pair_at(u + 1));
         __syncthreads();
         if (!K::P0R && kp == 0) {                         // block-uniform
             // remove_dc_bias (src/blur_profile.c:233-238): a constant per image only
@@ -486,7 +521,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
             }
         }
         // the next column's pass-0 inputs (p0v is free from here to the next step)
-        if (K::P0R && u + 1 < c1 && !(ablate & 4)) fetch0(pair_at(u + 1));
+        if (K::P0R && u + 1 < un && !(ablate & 4)) fetch0(pair_at(u + 1));
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
@@ -505,6 +540,14 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         fmax_part[blockIdx.x] = m;
     }
     if (!K::GB && !(ablate & 8)) flush_bins(lb, nbins, win, nr, bin_sums, tid, NT);
+    if (seg < c1) {
+        // the next image's bins start from zero (each thread clears the entries
+        // it flushed); red (in the buffer) is free after this barrier
+        if (!K::GB)
+            for (int i = tid; i < nbins; i += NT) lb[i] = 0ull;
+        __syncthreads();
+    }
+    }
 }
 
 template <typename K>
@@ -527,14 +570,15 @@ int resident_grid(K kernel, int threads, size_t lds) {
 
 template <int W, int T, int... Rs>
 hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, const double* k255,
-                   const double2* tw, double2* inter, unsigned long long* rsum, hipStream_t st) {
+                   const double2* tw, double2* inter, unsigned long long* rsum, hipStream_t st,
+                   const uint8_t* const* imgs = nullptr, int nimg = 1, long istride = 0) {
     const size_t lds = RowK<W, T, Rs...>::lds;
     static const int grid = [&] {
         const int g = resident_grid(k_rows_ct<W, T, Rs...>, T, lds) / 32 * 32;   // schedule needs % 32
         return g > 32 ? g : 32;
     }();
     phd_launch((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
-                       g_ablate, rsum);
+                       g_ablate, rsum, imgs, nimg, istride);
     return hipGetLastError();
 }
 
@@ -558,11 +602,13 @@ int cols_grid(int, int nbins) {
 template <int H, int T, int CPB, int... Rs>
 hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, unsigned long long* bin_sums,
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
-                   hipStream_t st) {
+                   hipStream_t st, int nimg = 1, long istride = 0, long bstride = 0, long fstride = 0,
+                   long sstride = 0) {
     const size_t lds = cols_lds<H, T, CPB, Rs...>(cb.nlb);
     const int grid = cb.grid > 0 ? cb.grid : cols_grid<H, T, CPB, Rs...>(wf, cb.nlb);
     phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.map, cb.nlb,
-               cb.win, cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate);
+               cb.win, cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg, istride,
+               bstride, fstride, sstride);
     return hipGetLastError();
 }
 
@@ -693,6 +739,36 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 #define PHD_X(N, V, T, ...) \
     if (n_ == N && V == v_) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, rsum, st);
     PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
+#undef PHD_X
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_fft_rows_ct_batch(const uint8_t* const* d_imgs, int n, int height, int width, const double* k255,
+                                    const double2* tw, double2* inter, long inter_stride, hipStream_t st) {
+    if (n < 1 || ((height + 1) / 2) % 4 != 0) return hipErrorInvalidValue;   // whole line groups per image
+    const int n_ = width;
+#define PHD_X(N, V, T, ...)                                                                                  \
+    if (n_ == N && V == v_)                                                                                  \
+        return rows_ct<N, T, __VA_ARGS__>(nullptr, height, nullptr, k255, tw, inter, nullptr, st, d_imgs, n, \
+                                          inter_stride);
+    PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
+#undef PHD_X
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int n, int height, int width, int wf,
+                                    const ColBins& cb, unsigned long long* bin_sums, long bin_stride,
+                                    double* fmax_part, long fmax_stride, const double2* tw,
+                                    const unsigned long long* sums, long sums_stride, hipStream_t st) {
+    // bin windows are made for one image's column owners (the batch spreads
+    // each image's columns over other blocks)
+    if (n < 1 || (cb.win && n > 1)) return hipErrorInvalidValue;
+    const int n_ = height;
+#define PHD_X(N, V, T, ...)                                                                                    \
+    if (n_ == N && V == v_)                                                                                    \
+        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, nullptr, st, n, \
+                                          inter_stride, bin_stride, fmax_stride, sums_stride);
+    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return hipErrorInvalidValue;
 }

@@ -361,8 +361,11 @@ static const ColWin* get_col_windows(Context* c, const BlurTable& t, int width) 
     return nullptr;
 }
 
+// batch: the caller will run the compile-time passes as batched launches,
+// whose blocks take different columns of each image, so no per-block bin
+// windows (they are made for one image's column owners)
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
-                const BlurTable* tbl) {
+                const BlurTable* tbl, bool batch) {
     *s = FftSel{};
     static const bool force_generic = getenv("PHD_FFT_GENERIC") != nullptr;   // A/B experiments only
     bool ct = !force_generic && ct_rows_plan(width, nullptr) && ct_cols_plan(height, nullptr) &&
@@ -374,7 +377,7 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         s->tw_r = get_ct_twiddles(c, width, true);
         s->tw_c = get_ct_twiddles(c, height, false);
         if (!s->tw_r || !s->tw_c) return false;
-        const ColWin* w = tbl ? get_col_windows(c, *tbl, width) : nullptr;
+        const ColWin* w = (tbl && !batch) ? get_col_windows(c, *tbl, width) : nullptr;
         if (w) {
             s->cbins = ColBins{w->d_lmap, w->d_win, w->win_max, tbl->nr, w->grid};
             s->col_blocks = w->grid;

@@ -297,7 +297,7 @@ struct FftSel {
 // tbl: the polar-bin table of the size (the compile-time column pass's bin
 // windows are made from it; nullptr: every block sums all na * nr bins)
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
-                const BlurTable* tbl);
+                const BlurTable* tbl, bool batch = false);
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,
                            const unsigned long long* sums, const double* k255, double2* inter, hipStream_t st,
                            unsigned long long* rsum = nullptr);

@@ -257,7 +257,15 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(6000, 0, 512, 6, 10, 10, 10)  \
     X(6000, 1, 768, 6, 10, 10, 10)  \
     X(3000, 0, 384, 5, 6, 10, 10)   \
-    X(2000, 0, 256, 5, 4, 10, 10)
+    X(2000, 0, 256, 5, 4, 10, 10)   \
+    /* config 5's sizes below 3 MP (round 3; batched launches, launch_fft_rows_ct_batch) */ \
+    X(2048, 0, 256, 8, 16, 16)      \
+    X(1920, 0, 256, 15, 8, 16)      \
+    X(1280, 0, 256, 5, 16, 16)      \
+    X(720, 0, 192, 5, 9, 16)        \
+    X(640, 0, 128, 5, 8, 16)        \
+    X(480, 0, 128, 5, 6, 16)        \
+    X(512, 0, 64, 8, 8, 8)
 // columns: X(length, variant, threads per column, flags, radices...); flags:
 // columns per block (1, 2) | 4 no register prefetch | 8 bins by global atomics.
 // Measured at 4000x3000 (tools/ct_sweep.py): v0 54.8 us, v2 55.5, v3 56.0,
@@ -293,7 +301,15 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(6000, 1, 512, 5, 10, 20, 30)     \
     X(4000, 0, 256, 5, 10, 20, 20)     \
     X(4000, 1, 320, 5, 10, 20, 20)     \
-    X(2000, 0, 256, 5, 10, 10, 20)
+    X(2000, 0, 256, 5, 10, 10, 20)     \
+    /* config 5's sizes below 3 MP (round 3; batched launches, launch_fft_cols_ct_batch) */ \
+    X(1536, 0, 256, 5, 3, 8, 8, 8)     \
+    X(1080, 0, 192, 5, 15, 8, 9)       \
+    X(1280, 0, 256, 5, 5, 16, 16)      \
+    X(720, 0, 192, 5, 5, 9, 16)        \
+    X(640, 0, 128, 5, 5, 8, 16)        \
+    X(480, 0, 128, 5, 5, 6, 16)        \
+    X(512, 0, 64, 5, 8, 8, 8)
 int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);
@@ -332,6 +348,17 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const ColBins& cb,
                               unsigned long long* bin_sums, double* fmax_part, const double2* tw,
                               const unsigned long long* sums, double* dbg, hipStream_t st);
+// Batches of n images of one size in one launch each (sizes whose row pairs
+// form whole line groups, (height + 1) / 2 % 4 == 0): d_imgs is a device array
+// of image pointers; image i's intermediate, bin sums, max partials and channel
+// sums sit i * inter_stride / bin_stride / fmax_stride / sums_stride elements
+// from the first.  Small images are otherwise bound by per-launch costs.
+hipError_t launch_fft_rows_ct_batch(const uint8_t* const* d_imgs, int n, int height, int width, const double* k255,
+                                    const double2* tw, double2* inter, long inter_stride, hipStream_t st);
+hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int n, int height, int width, int wf,
+                                    const ColBins& cb, unsigned long long* bin_sums, long bin_stride,
+                                    double* fmax_part, long fmax_stride, const double2* tw,
+                                    const unsigned long long* sums, long sums_stride, hipStream_t st);
 // Same, the luma from an fp64 plane when pgm != nullptr (planar input).
 hipError_t launch_sharpness_src(const uint8_t* img, const double* pgm, int height, int width, int n, const int* top,
                                 const int* bottom, const int* left, const int* right, const double* k255,

@@ -27,6 +27,12 @@
 
 namespace phd {
 
+// PHD_FFT_OVERLAP=1 (compile-time plans): see run_reports
+static bool overlap_env() {
+    static const bool v = getenv("PHD_FFT_OVERLAP") != nullptr;
+    return v;
+}
+
 namespace {
 
 constexpr size_t kAlign = 256;
@@ -461,7 +467,16 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const BlurTable* tbl = get_table(c, height, width, cfg.radius_partitions, cfg.angle_partitions);
     if (!tbl) return false;
     FftSel fs;
-    if (!select_fft(c, height, width, nbins, d_imgs, n, &fs, tbl)) return false;
+    // compile-time plans: images small enough that two or more half-spectrum
+    // intermediates fit 128 MB (half the MALL) run as one row and one column
+    // launch per group of images (sizes whose row pairs form whole line groups
+    // of the row schedule); small images are otherwise bound by per-launch costs
+    const size_t inter_one = sizeof(double2) * ((size_t)(height + 1) * (wf + 1) + 1024);
+    static const bool ctbatch_off = getenv("PHD_CT_NO_BATCH") != nullptr;
+    const int q_ct = (int)std::min<size_t>((size_t)n, ((size_t)128 << 20) / inter_one);
+    const bool ct_batchable = !ctbatch_off && !overlap_env() && !getenv("PHD_FFT_PIPE") && n > 1 && q_ct >= 2 &&
+                              ((height + 1) / 2) % 4 == 0;
+    if (!select_fft(c, height, width, nbins, d_imgs, n, &fs, tbl, ct_batchable)) return false;
     const Context::Cls* cls = get_cls(c, gp);
     if (!cls) return false;
 
@@ -482,7 +497,6 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // half-spectrum intermediates: one per image of a group of Q (the group's row
     // passes run before its column passes; measured best at Q = 1)
     // (+ 1024 elements of scratch past the tiles for the row pass's dummy stores)
-    const size_t inter_one = sizeof(double2) * ((size_t)(height + 1) * (wf + 1) + 1024);
     static const int qcap = getenv("PHD_FFT_GROUP") ? atoi(getenv("PHD_FFT_GROUP")) : 0;
     int Q = std::min(n, qcap > 0 ? qcap : 1);   // 1: the intermediate stays in the 256 MB MALL
     while (Q > 1 && (size_t)Q * inter_one > ((size_t)2 << 30)) Q = (Q + 1) / 2;
@@ -497,7 +511,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     static const bool gbatch_off = getenv("PHD_FFT_NO_BATCH") != nullptr;
     const bool gbatch = !fs.ct && !fs.generic && !gbatch_off && n > 1 && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
     if (gbatch) Q = std::max(1, std::min(n, (int)(((size_t)128 << 20) / inter_one)));
-    const bool pipe = !gbatch && !fs.generic && Q == 1 && n > 1 && pipe_env;
+    const bool ctbatch = fs.ct && ct_batchable && !fs.cbins.win && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
+    if (ctbatch) Q = q_ct;
+    const bool pipe = !gbatch && !ctbatch && !fs.generic && Q == 1 && n > 1 && pipe_env;
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)(pipe ? 2 : Q) * inter_one))
         return false;
@@ -544,8 +560,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // default the FFTs follow K1 (and its records' download) on K1's stream and
     // take its channel sums: a cross-stream event wait left the GPU idle
     // ~20 us between K1 and the first row pass.
-    static const bool overlap = getenv("PHD_FFT_OVERLAP") != nullptr;
-    const bool own_dc = fs.ct && overlap;
+    const bool own_dc = fs.ct && overlap_env();
     const hipStream_t sf = (pipe || own_dc) ? c->fft : st;
     if (sf != st) {
         PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
@@ -605,7 +620,30 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             if (dl_end(i)) PHD_HIP(hipEventRecord(c->ev_img_fft[i], sf));
         }
     }
-    for (int g0 = 0; g0 < (pipe || gbatch ? 0 : n); g0 += Q) {
+    for (int g0 = 0; ctbatch && g0 < n; g0 += Q) {
+        const int g1 = std::min(n, g0 + Q);
+        const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(n));
+        int ps = c->prof.begin(kFftRows, sf);
+        PHD_HIP(launch_fft_rows_ct_batch(d_ptrs + g0, g1 - g0, height, width, c->d_k255, fs.tw_r, c->d_inter,
+                                         (long)inter_elems, sf));
+        c->prof.end(ps, sf);
+        ps = c->prof.begin(kFftCols, sf);
+        PHD_HIP(launch_fft_cols_ct_batch(c->d_inter, (long)inter_elems, g1 - g0, height, width, wf, fs.cbins,
+                                         (unsigned long long*)(dw + L.C(n, g0) + L.c_bins), (long)(L.c_bytes / 8),
+                                         (double*)(dw + L.C(n, g0) + L.c_fmax), (long)(L.c_bytes / 8), fs.tw_c,
+                                         (const unsigned long long*)(dw + L.A(g0) + L.a_sums), (long)(L.a_bytes / 8),
+                                         sf));
+        c->prof.end(ps, sf);
+        for (int i = g0; i < g1; i++) {
+            if (ncrops)
+                PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
+                                         crop_arr.data() + ncrops, crop_arr.data() + 2 * ncrops,
+                                         crop_arr.data() + 3 * ncrops, c->d_k255,
+                                         (double*)(dw + L.C(n, i) + L.c_sharp), sf));
+            if (dl_end(i)) PHD_HIP(hipEventRecord(c->ev_img_fft[i], sf));
+        }
+    }
+    for (int g0 = 0; g0 < (pipe || gbatch || ctbatch ? 0 : n); g0 += Q) {
         const int g1 = std::min(n, g0 + Q);
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
@@ -878,6 +916,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         printf("color palette decisions alone (%d images) took %f seconds to execute \n", n,
                ms(t_k1, t_dec_only) / 1e3);
         printf("palette tail and download enqueue took %f seconds to execute \n", ms(t_dec_only, t_dec) / 1e3);
+        printf("palette tail: %d partial-group entries, at most %d per image\n", n_ent, max_per_img);
     }
     return failures == 0;
 }
@@ -1595,6 +1634,14 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
         void* p;
         ~FreeOnExit() { if (p) (void)hipFree(p); }
     } free_scratch{fscratch};
+    // the column pass's bins and per-block max partials: a buffer of their own
+    // (a small image's workspace is smaller than a persistent grid's partials)
+    const int nbins = cfg->radius_partitions * cfg->angle_partitions;
+    void* cscratch = nullptr;
+    if (kernel == kFftCols &&
+        hipMalloc(&cscratch, sizeof(double) * ((size_t)nbins + std::max(4096, fs.col_blocks))) != hipSuccess)
+        return -1;
+    FreeOnExit free_cscratch{cscratch};
     const uint8_t** d_ptr = nullptr;
     if (!ensure_device((void**)&c->d_ptrs, &c->ptrs_bytes, sizeof(void*))) return -1;
     d_ptr = (const uint8_t**)c->d_ptrs;
@@ -1614,10 +1661,9 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
                                                     all_aligned(&d_rgb, 1), st);
                 break;
             case kFftRows: e = launch_rows_sel(fs, d_rgb, height, width, pd.sums, c->d_k255, c->d_inter, st); break;
-            case kFftCols: e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map,
-                                               cfg->radius_partitions * cfg->angle_partitions,
-                                               (unsigned long long*)pd.chunk_hist,
-                                               (double*)pd.chunk_hist + 65536, pd.sums, nullptr, st); break;
+            case kFftCols: e = launch_cols_sel(fs, c->d_inter, height, width, wf, tbl->d_map, nbins,
+                                               (unsigned long long*)cscratch, (double*)cscratch + nbins, pd.sums,
+                                               nullptr, st); break;
             default: set_error("kernel not supported by the timing hook"); g_ablate = 0; return -1;
         }
         if (e != hipSuccess) {
@@ -1682,7 +1728,7 @@ extern "C" int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int wi
     uint8_t* dw = (uint8_t*)c->d_ws;
     const int wf = width / 2 + 1;
     double* scratch = nullptr;
-    if (hipMalloc(&scratch, sizeof(double) * (nbins + 4096)) != hipSuccess) return -1;
+    if (hipMalloc(&scratch, sizeof(double) * (nbins + std::max(4096, fs.col_blocks))) != hipSuccess) return -1;
     auto* scratch_bins = reinterpret_cast<unsigned long long*>(scratch);
     const hipStream_t st = c->stream;
     hipError_t e = launch_rows_sel(fs, d_rgb, height, width, (const unsigned long long*)dw, c->d_k255, c->d_inter, st);

@@ -497,14 +497,18 @@ def test_fused_palette_sums_against_oracle(cfg, kind):
     np.testing.assert_allclose(np.array(cp.hsv).reshape(-1, 3), o["palette_hsv"], rtol=TIGHT_RTOL, atol=1e-12)
 
 
-@pytest.mark.parametrize("kind,seed", [("uniform", 5), ("structured", 6)])
-def test_power_spectrum_compile_time_fft_4000x3000(kind, seed):
+@pytest.mark.parametrize("kind,seed,H,W", [("uniform", 5, 3000, 4000), ("structured", 6, 3000, 4000),
+                                            # config 5's sub-3-MP sizes (compile-time plans, round 3)
+                                            ("structured", 7, 1080, 1920),
+                                            ("structured", 9, 1536, 2048), ("uniform", 10, 720, 1280),
+                                            ("structured", 11, 1280, 720), ("uniform", 12, 640, 480),
+                                            ("structured", 13, 480, 640), ("structured", 14, 512, 512)])
+def test_power_spectrum_compile_time_fft(kind, seed, H, W):
     """The production FFT kernels' |X|^2 against numpy's rfft2 (pocketfft, fp64)
     of the reference's luma - DC bias (src/image_processing.c:505-512,
     src/blur_profile.c:233-238, src/fft_processing.c:34-50)."""
     phd, L, torch = _phd()
     from photohive_dsp_amd import synth
-    H, W = 3000, 4000
     img = synth.make(kind, H, W, seed)
     t = torch.from_numpy(np.ascontiguousarray(img)).cuda()
     wf = W // 2 + 1

@@ -79,3 +79,28 @@ def test_mixed_batch_groups_past_64_images():
         np.testing.assert_allclose(np.array(r.color_palette.hsv), np.array(one.color_palette.hsv), rtol=1e-12)
         assert np.array_equal(np.array(r.blur_profile.bins), np.array(one.blur_profile.bins))
         assert r.blur_vectors == one.blur_vectors
+
+
+@pytest.mark.parametrize("shape,n", [((1080, 1920), 5), ((1536, 2048), 3), ((720, 1280), 5), ((1280, 720), 5),
+                                     ((640, 480), 5), ((480, 640), 5), ((512, 512), 70)])
+def test_compile_time_fft_batches_match_single_reports(shape, n):
+    """Config 5's sub-3-MP sizes take compile-time plans, one row and one column
+    launch per group of images (launch_fft_*_ct_batch; 70 images of 512x512 make
+    two groups).  Every image's bins (fixed point) and blur vectors are
+    bit-identical to its single-image report's, which runs the per-image
+    kernels, and its palette is the same."""
+    L, torch = _lib()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import report_device
+    h, w = shape
+    kinds = ("structured", "uniform", "dominant", "hblur", "motion")
+    imgs = np.stack([synth.make(kinds[i % 5], h, w, 300 + i) for i in range(n)])
+    t = torch.from_numpy(imgs).cuda()
+    reps = report_device(t)
+    for i in sorted({0, 1, n // 2, n - 2, n - 1}):
+        one = report_device(t[i:i + 1].contiguous())[0]
+        r = reps[i]
+        assert np.array_equal(np.array(r.blur_profile.bins), np.array(one.blur_profile.bins)), i
+        assert r.blur_vectors == one.blur_vectors, i
+        assert r.color_palette.group_ids == one.color_palette.group_ids, i
+        assert r.color_palette.quantities == one.color_palette.quantities, i
