@@ -104,3 +104,28 @@ def test_compile_time_fft_batches_match_single_reports(shape, n):
         assert r.blur_vectors == one.blur_vectors, i
         assert r.color_palette.group_ids == one.color_palette.group_ids, i
         assert r.color_palette.quantities == one.color_palette.quantities, i
+
+
+_BATCHED_FIXTURES = ("structured_640x480_hsv36", "hblur_480x640", "vblur_480x640", "dominant_1280x720_hsv36",
+                     "structured_1080x1920_L5000", "uniform_1536x2048_hsv36", "uniform_512_hsv36_4_5")
+
+
+@pytest.mark.parametrize("name", _BATCHED_FIXTURES)
+def test_compile_time_fft_batches_match_reference_fixtures(name):
+    """The batched compile-time FFT launches (three copies of a golden image in
+    one device batch, so one row and one column launch cover all three) against
+    the reference's own outputs for that image, at the same bars as the
+    single-image fixture test."""
+    from tests.conftest import golden_case, golden_image, golden_manifest
+    from tests.test_gpu_parity import BINS_NORMWISE, assert_report_matches
+    from photohive_dsp_amd.core import report_device
+    L, torch = _lib()
+    case = next(c for c in golden_manifest()["cases"] if c["name"] == name)
+    assert not case["crops"] and not case["config"].get("downsample_rate")
+    g = golden_case(name)
+    img = np.ascontiguousarray(golden_image(case))
+    t = torch.from_numpy(np.stack([img] * 3)).cuda()
+    for rep in report_device(t, **case["config"]):
+        assert_report_matches(rep, g)
+        bins = np.array(rep.blur_profile.bins)
+        assert np.max(np.abs(bins - g["bins"])) <= BINS_NORMWISE * max(np.max(np.abs(g["bins"])), 1e-300)
