@@ -226,12 +226,6 @@ __device__ __forceinline__ void t_exact(int kr, int kg, int kb, const double* k2
     atomicAdd(a + 1, s);
 }
 
-// byte k (< 12) of a 4-pixel group's three words
-__device__ __forceinline__ int group_byte(unsigned a0, unsigned a1, unsigned a2, int k) {
-    const unsigned w = k < 4 ? a0 : (k < 8 ? a1 : a2);
-    return (int)((w >> (8 * (k & 3))) & 255u);
-}
-
 struct Mom {
     unsigned sr, sg, sb, qr, qg, qb;
 };
@@ -398,25 +392,24 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             }
         }
         // deferred pixels (a hue exactly on a half-bin boundary, ~1.7 % of uniform
-        // pixels): the thread counts its own in fp64 from the chunk words it still
-        // holds (no LDS queue, no extra barrier; measured the same time as the
-        // queue resolved by the whole block, and as a 4 MiB decision table; a
+        // pixels): the thread counts its own in fp64, re-reading the pixel from
+        // global memory (no LDS queue, no extra barrier; measured the same time as
+        // the queue resolved by the whole block, and as a 4 MiB decision table; a
         // per-wave queue filled by a lane scan, round 3, 2.55 against 2.51 ms per
-        // 64-image launch: its extra registers doubled the VGPR spills)
+        // 64-image launch: its extra registers doubled the VGPR spills).  The
+        // re-read instead of selecting the pixel from the chunk's words, which then
+        // had to stay live through the whole chunk: 9.98 -> 9.86 ms per 256-image
+        // launch (20 -> 15 VGPRs spilled in the 512-thread form); a rolling
+        // prefetch (group st of the next chunk loaded as group st of this one is
+        // consumed) on top of it measured 10.27 ms (31 spilled)
         while (emask) {
             const int bt = __ffs(emask) - 1;
             emask &= emask - 1;
             const int gst = bt >> 2, pi = bt & 3;
-            unsigned a0 = 0, a1 = 0, a2 = 0;
-#pragma unroll
-            for (int st = 0; st < kG; st++)
-                if (st == gst) {
-                    a0 = cw[st][0];
-                    a1 = cw[st][1];
-                    a2 = cw[st][2];
-                }
-            t_exact<TRI>(group_byte(a0, a1, a2, 3 * pi), group_byte(a0, a1, a2, 3 * pi + 1),
-                    group_byte(a0, a1, a2, 3 * pi + 2), k255, gp, code8, inv, cells, gs2, X);
+            // re-read the pixel (L2-resident: its chunk was just loaded) instead of
+            // keeping the chunk's words live through the classification
+            const uint8_t* q = cip + 3 * (base + 4L * tid + 4L * kT * gst + pi);
+            t_exact<TRI>(q[0], q[1], q[2], k255, gp, code8, inv, cells, gs2, X);
         }
         const long pad = base + kChunk - full_end;                // zero pixels of masked groups
         if (pad > 0 && tid == 0) atomicAdd(&cells[zcell << cshift], (unsigned long long)(-pad));
