@@ -128,7 +128,7 @@ struct TRead {
     int code;
     double ikd, imx;
 };
-// The pixel's three table reads (issued for a whole 4-pixel group before its
+// The pixel's three table reads (issued for PHD_K1_RDB pixels of a group before their
 // atomics: LDS operations complete in order, so a read placed after an atomic
 // would wait for it).
 template <bool TRI>
@@ -264,19 +264,30 @@ __device__ __forceinline__ unsigned t_group(unsigned w0, unsigned w1, unsigned w
     const unsigned Mx[2] = {M02, M13}, Mn[2] = {N02, N13};
     unsigned def = 0;
     if (abl & 32) return 0;
-    TRead rd[4];
+    // the table reads of two pixels are issued before their atomics (LDS
+    // operations complete in order, so a read placed after an atomic waits for
+    // it); four at a time held 20 more VGPRs and the 512-thread form spilled
+    // 15 of them: 9.87 -> 9.78 ms per 256-image launch with two (round 3)
+#ifndef PHD_K1_RDB
+#define PHD_K1_RDB 2
+#endif
+    constexpr int RB = PHD_K1_RDB;                              // pixels whose table reads are batched
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int q = i & 1, sh = 16 * (i >> 1);               // pixel i: pair q, half i >> 1
-        const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF;
-        rd[i] = t_read<TRI>(kmx, kmx - kmn, code8, inv);
-    }
+    for (int i0 = 0; i0 < 4; i0 += RB) {
+        TRead rd[RB];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int q = i & 1, sh = 16 * (i >> 1);
-        const int kr = (R[q] >> sh) & 0xFFFF, kg = (G[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
-        const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF;
-        def |= (unsigned)t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, rd[i], cells, gs2, X, abl) << i;
+        for (int i = i0; i < i0 + RB; i++) {
+            const int q = i & 1, sh = 16 * (i >> 1);           // pixel i: pair q, half i >> 1
+            const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF;
+            rd[i - i0] = t_read<TRI>(kmx, kmx - kmn, code8, inv);
+        }
+#pragma unroll
+        for (int i = i0; i < i0 + RB; i++) {
+            const int q = i & 1, sh = 16 * (i >> 1);
+            const int kr = (R[q] >> sh) & 0xFFFF, kg = (G[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
+            const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF;
+            def |= (unsigned)t_pixel(kr, kg, kb, kmx, kmn, kmx - kmn, rd[i - i0], cells, gs2, X, abl) << i;
+        }
     }
     return def;
 }
