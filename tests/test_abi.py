@@ -81,10 +81,10 @@ def test_every_field_offset_matches_reference_structures():
 @pytest.mark.skipif(not os.path.exists("/root/reference/structures.py"),
                     reason="the reference tree exists only in the build container")
 def test_field_offsets_match_live_reference_structures():
-    """The same comparison against the reference's structures.py itself, loaded
-    by importlib (no other reference module is imported)."""
-    from tests.golden.make_struct_layout import layout, load_reference
-    ref = layout(load_reference())
+    """The same comparison against the reference's structures.py itself, read
+    with `ast` (its `_fields_` literals; the file is never executed)."""
+    from tests.golden.make_struct_layout import layout, parse_reference
+    ref = layout(parse_reference())
     ours = _our_layout()
     for name, want in ref.items():
         assert ours.get(name) == want, (name, ours.get(name), want)
@@ -141,3 +141,16 @@ def test_lanes_setting_and_batch_free_need_no_gpu():
     lib.phd_free_reports(outs, 3)
     lib.phd_free_reports(None, 0)
     assert all(not outs[i] for i in range(3))
+
+
+def test_gpurunignore_keeps_reference_builds_off_the_gpu_box():
+    """reference sources and anything built from them
+    never go to the GPU box.  oracle/Makefile writes the reference build into
+    oracle/_ref/ (from REF_SRC) and the sanitizer build into oracle/_san/;
+    both directories must be excluded from every gpurun snapshot."""
+    ign = [l.strip() for l in open(os.path.join(ROOT, ".gpurunignore")) if l.strip() and not l.startswith("#")]
+    mk = open(os.path.join(ROOT, "oracle", "Makefile")).read()
+    outdirs = sorted(set(re.findall(r"\$\(HERE\)(_[a-z]+)/", mk)))
+    assert "_ref" in outdirs and "_san" in outdirs, outdirs
+    for d in outdirs:
+        assert f"./oracle/{d}" in ign or f"oracle/{d}" in ign, (d, ign)
