@@ -107,7 +107,11 @@ Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundaries* salien
  * and sets *report = NULL.  A report of this library is one heap block (every
  * structure and array of the tree inside it), recycled for later reports of
  * the same size; release it only through this call (as the reference's
- * callers do), never by free() on its members. */
+ * callers do), never by free() on its members (a documented deviation: the
+ * reference mallocs each member, src/interface.c:97-111).  A pointer that is
+ * not a live report of this library (foreign, or already freed and not yet
+ * reused) is ignored; freeing a stale pointer after its block was reused by a
+ * later report is undefined, as with free(). */
 void free_full_report(Full_Report_Data** report);
 /* free_full_report over an array of n reports (a batch call's `out`); NULL entries are skipped. */
 void phd_free_reports(Full_Report_Data** reports, int n);

@@ -22,6 +22,7 @@
 #include <thread>
 #include <unistd.h>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "phd_host.h"
 
@@ -166,48 +167,68 @@ namespace {
 // page faults between batches) cost ~0.9 ms per batch with the GPU idle.
 constexpr size_t kReportHdr = 16;
 constexpr unsigned long long kReportMagic = 0x5048445245504f52ull;   // "PHDREPOR"
+// The pool also keeps the set of blocks that are live reports: free_full_report
+// pools a block only if it is in that set, so a pointer this library did not
+// return (or a report already freed and not yet handed out again) is ignored
+// without reading memory around it.  A stale pointer to a block that a later
+// report has taken again cannot be told from that report (as with free()):
+// freeing it twice after such a reuse is undefined.
 struct ReportPool {
+    pid_t pid = 0;                                           // the process that made this pool
     std::mutex m;
     std::unordered_map<size_t, std::vector<void*>> blocks;   // by block size
+    std::unordered_set<const void*> live;                    // blocks handed out as reports
     size_t bytes = 0;
     static constexpr size_t kCap = (size_t)512 << 20;        // pooled bytes at most
     void* take(size_t sz) {
+        void* b = nullptr;
         {
             std::lock_guard<std::mutex> lk(m);
             auto it = blocks.find(sz);
             if (it != blocks.end() && !it->second.empty()) {
-                void* b = it->second.back();
+                b = it->second.back();
                 it->second.pop_back();
                 bytes -= sz;
-                return b;
             }
         }
-        return malloc(sz);
+        if (!b) b = malloc(sz);
+        if (b) {
+            std::lock_guard<std::mutex> lk(m);
+            live.insert(b);
+        }
+        return b;
     }
-    void give(void* b, size_t sz) {
+    // returns false (and leaves the block alone) when b is not a live report
+    bool give(void* b) {
         std::lock_guard<std::mutex> lk(m);
+        if (!live.erase(b)) return false;
+        const size_t sz = (size_t)reinterpret_cast<unsigned long long*>(b)[0];
+        reinterpret_cast<unsigned long long*>(b)[1] = 0;
         if (bytes + sz > kCap) {
             free(b);
-            return;
+            return true;
         }
         blocks[sz].push_back(b);
         bytes += sz;
+        return true;
     }
 };
 ReportPool& report_pool() {
-    // process lifetime (reports may be freed at exit); a forked child starts
-    // a pool of its own (the parent's mutex may have been held at the fork)
+    // process lifetime (reports may be freed at exit); a forked child starts a
+    // pool of its own (the parent's mutex may have been held at the fork).  One
+    // pointer holds both the pool and the pid that made it, so a thread cannot
+    // pair one process's pool with another's pid.
     static std::atomic<ReportPool*> p{nullptr};
-    static std::atomic<pid_t> owner{0};
-    ReportPool* q = p.load();
-    if (!q || owner.load() != getpid()) {
+    ReportPool* q = p.load(std::memory_order_acquire);
+    const pid_t me = getpid();
+    if (!q || q->pid != me) {
         static std::mutex init;
         std::lock_guard<std::mutex> lk(init);
-        q = p.load();
-        if (!q || owner.load() != getpid()) {
+        q = p.load(std::memory_order_acquire);
+        if (!q || q->pid != me) {
             q = new ReportPool;
-            p.store(q);
-            owner.store(getpid());
+            q->pid = me;
+            p.store(q, std::memory_order_release);
         }
     }
     return *q;
@@ -259,7 +280,7 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
             *why = "palette self-check failed: device kept " + std::to_string((long long)cnt) +
                    " pixels for slot " + std::to_string(k) + ", host rules predict " +
                    std::to_string(dec.kept[k]);
-            report_pool().give(blk, size);
+            report_pool().give(blk);
             return nullptr;
         }
         const int tot = (int)dec.kept[k];
@@ -1106,14 +1127,12 @@ extern "C" void phd_free_reports(Full_Report_Data** reports, int n) {
 
 extern "C" void free_full_report(Full_Report_Data** report) {
     // src/interface.c:97-111 frees each structure; every report of this
-    // library is one block (assemble), which goes back to the report pool
+    // library is one block (assemble), which goes back to the report pool.
+    // Not a live report of this library (foreign, or already freed): ignored.
     if (!report || !*report) return;
     char* blk = reinterpret_cast<char*>(*report) - kReportHdr;
-    unsigned long long* h = reinterpret_cast<unsigned long long*>(blk);
-    if (h[1] == kReportMagic) {
-        h[1] = 0;                                  // a second free of this block is a no-op
-        report_pool().give(blk, (size_t)h[0]);
-    }
+    if (!report_pool().give(blk) && getenv("PHD_VERBOSE"))
+        fprintf(stderr, "free_full_report: %p is not a live report of this library; ignored\n", (void*)*report);
     *report = nullptr;
 }
 

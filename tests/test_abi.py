@@ -154,3 +154,21 @@ def test_gpurunignore_keeps_reference_builds_off_the_gpu_box():
     assert "_ref" in outdirs and "_san" in outdirs, outdirs
     for d in outdirs:
         assert f"./oracle/{d}" in ign or f"oracle/{d}" in ign, (d, ign)
+
+
+def test_free_full_report_ignores_foreign_pointers():
+    """Reports are single pooled blocks (include/photohive_dsp.h): the library
+    pools only blocks it handed out, so freeing a structure it did not
+    allocate touches nothing around it and still clears the caller's pointer;
+    a NULL report is a no-op (the reference would dereference it)."""
+    from photohive_dsp_amd.lib import lib
+    from photohive_dsp_amd.structures import Full_Report_Data
+    guard = (ctypes.c_ubyte * 128)(*([0xAB] * 128))
+    foreign = Full_Report_Data.from_buffer(guard, 32)
+    p = ctypes.pointer(foreign)
+    lib.free_full_report(ctypes.byref(p))
+    assert not p                                    # *report = NULL
+    assert all(b == 0xAB for b in guard)            # no header read or write around it
+    null = ctypes.POINTER(Full_Report_Data)()
+    lib.free_full_report(ctypes.byref(null))
+    lib.phd_free_reports(None, 3)
