@@ -15,7 +15,7 @@ A step = one full report (stats, S-bar, palette, blur profile, blur vectors)
 of every image of one device-resident batch of B images per GPU.  Images are
 synthetic (splitmix64 uniform RGB8, generated on the device; seed = global
 image index).  Ranks shard images with no data-path collective; one small
-all-gather merges the counters (shard.merge_counters).  Rank 0 prints one
+all-reduce merges the counters (shard.merge_counters).  Rank 0 prints one
 JSON line.
 """
 from __future__ import annotations

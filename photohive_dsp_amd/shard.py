@@ -3,8 +3,9 @@
 Images are independent and each fits one GPU, so the batch is partitioned
 across ranks with no data-path collective: every rank reports on its own
 images and keeps its results.  The only collective merges a few counters
-(images, pixels, wall time) -- a sum for counts and a max for time -- over
-RCCL (backend "nccl") on the GPU box or gloo in the CPU tests.
+(images, pixels, wall time) -- one all-reduce SUM whose wall-time slots are
+one-hot per rank, so the max is taken after it -- over RCCL (backend "nccl")
+on the GPU box or gloo in the CPU tests.
 
 Mixed sizes (BASELINE.json config 5) are balanced with a static LPT
 assignment: images sorted by pixel count, largest first, each onto the
@@ -52,24 +53,27 @@ COUNTERS = ("elapsed", "images", "pixels", "alg_bytes", "kernel_ms", "launches")
 
 
 def merge_counters(values, device=None):
-    """The single collective: one all-gather of this rank's
+    """The single collective: ONE all-reduce (SUM) over the
+    default process group (RCCL over xGMI on the GPU box, gloo in the CPU
+    tests; identity when torch.distributed is not initialised) of this rank's
     counter vector {elapsed s, images, pixels, algorithmic bytes, kernel ms,
-    kernel launches} over the default process group (RCCL over xGMI on the GPU
-    box, gloo in the CPU tests; identity when torch.distributed is not
-    initialised).  Every rank gets the merge: the max of the wall times and the
-    sums of the rest, plus each rank's wall time (per_rank_elapsed)."""
+    kernel launches} followed by a one-hot row of world slots holding its wall
+    time at its rank.  Every rank gets the merge: the sums of the counters, the
+    max of the wall times (from the one-hot slots) and each rank's wall time
+    (per_rank_elapsed)."""
     import torch
     import torch.distributed as dist
     vals = [float(v) for v in values] + [0.0] * (len(COUNTERS) - len(values))
-    t = torch.tensor(vals, dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        out = torch.empty(dist.get_world_size() * len(COUNTERS), dtype=torch.float64, device=device)
-        dist.all_gather_into_tensor(out, t)
-        out = out.view(-1, len(COUNTERS))
-    else:
-        out = t[None]
-    rows = out.cpu().tolist()
-    res = {k: sum(r[j] for r in rows) for j, k in enumerate(COUNTERS)}
-    res["elapsed"] = max(r[0] for r in rows)
-    res["per_rank_elapsed"] = [r[0] for r in rows]
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    world, rank = (dist.get_world_size(), dist.get_rank()) if multi else (1, 0)
+    slots = [0.0] * world
+    slots[rank] = vals[0]
+    t = torch.tensor(vals + slots, dtype=torch.float64, device=device)
+    if multi:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    row = t.cpu().tolist()
+    res = {k: row[j] for j, k in enumerate(COUNTERS)}
+    per_rank = row[len(COUNTERS):]
+    res["elapsed"] = max(per_rank)
+    res["per_rank_elapsed"] = per_rank
     return res
