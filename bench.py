@@ -269,10 +269,34 @@ def cpu_baseline(h, w, topo, procs):
 def algorithmic_bytes(kernel, h, w):
     """Bytes one launch must move per image: RGB8 reads of the pixel
     passes, the fp64-complex half spectrum written by the row pass and read by the
-    column pass, which also reads the u16 polar-bin map (2 B per spectrum element)."""
+    column pass (its polar-bin runs, ~1.5 MB per size shared by every image, are
+    an implementation table, not counted)."""
     n, hwf = h * w, h * (w // 2 + 1)
     return {"hsv_stats": 3 * n, "palette_sums": 3 * n, "fft_rows": 3 * n + 16 * hwf,
-            "fft_cols": 18 * hwf, "report": 9 * n + 32 * hwf}.get(kernel)
+            "fft_cols": 16 * hwf, "report": 9 * n + 32 * hwf}.get(kernel)
+
+
+def per_kernel_roofline(warm, B, H, W):
+    """Each per-image pass's HBM fraction from the warm-up steps that bracket
+    its launches (one kernel per step): algorithmic bytes per
+    launch / average launch time / peak."""
+    out = {}
+    for name, v in warm.items():
+        per_launch = B / v["launches"]
+        ab = algorithmic_bytes(name, H, W) * per_launch
+        gbs = ab / (v["avg_us"] * 1e-6) / 1e9
+        out[name] = {"avg_launch_us": round(v["avg_us"], 2), "images_per_launch": per_launch,
+                     "us_per_image": round(v["avg_us"] / per_launch, 2),
+                     "algorithmic_bytes_per_image": algorithmic_bytes(name, H, W),
+                     "achieved_GB_per_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    return out
+
+
+def pipeline_roofline(images_per_s, H, W):
+    """The whole report against HBM: images/s x SURVEY.md 8(d)'s 9 N + 32 H Wf bytes."""
+    gbs = images_per_s * algorithmic_bytes("report", H, W) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_image": algorithmic_bytes("report", H, W)}
 
 
 class Ctx:
@@ -308,11 +332,15 @@ def kernel_times(lib, names):
     return out
 
 
-def headline(cx, timed_events=True):
+def headline(cx, timed_events=True, kind="uniform", steps=None):
     """Config 2, weak-scaled: B device-resident 4000x3000 images per rank per step.
     timed_events=False: no kernel events in the timed region (the warm-up
-    steps still time the candidates)."""
+    steps still time the candidates).  kind "hblur": SURVEY.md 8(d) row 2(b)'s
+    structured images (gradient + disks + 15-px horizontal box blur, synth.py,
+    generated on the device; seed 2 + global image index) instead of uniform
+    random bytes."""
     args, lib, torch = cx.args, cx.lib, cx.torch
+    steps = args.steps if steps is None else steps
     from photohive_dsp_amd.core import make_config
     from photohive_dsp_amd.lib import KERNELS
     from photohive_dsp_amd.structures import Full_Report_Data
@@ -320,7 +348,11 @@ def headline(cx, timed_events=True):
     img_bytes = H * W * 3
     d_imgs = torch.empty(B * img_bytes, dtype=torch.uint8, device="cuda")
     for i in range(B):
-        cx.fill(d_imgs[i * img_bytes:(i + 1) * img_bytes], cx.rank * B + i)
+        if kind == "hblur":
+            assert lib.phd_fill_structured_device(d_imgs[i * img_bytes:].data_ptr(), H, W, 2 + cx.rank * B + i, 15, 1,
+                                                  None) == 0, cx.last_error()
+        else:
+            cx.fill(d_imgs[i * img_bytes:(i + 1) * img_bytes], cx.rank * B + i)
     torch.cuda.synchronize()
     cfg = make_config()
     outs = (ctypes.POINTER(Full_Report_Data) * B)()
@@ -357,7 +389,7 @@ def headline(cx, timed_events=True):
     cx.barrier()
     t0 = time.perf_counter()
     stage = [0.0] * 8
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
         tm = (ctypes.c_double * 8)()
         lib.phd_last_timings(tm, 8)
@@ -367,14 +399,14 @@ def headline(cx, timed_events=True):
     elapsed = time.perf_counter() - t0
     kern = kernel_times(lib, KERNELS)
     lib.phd_profile_kernels(0)
-    n_img = B * args.steps
+    n_img = B * steps
     km = kern[dom]["total_ms"] if dom in kern else 0.0
     kl = kern[dom]["launches"] if dom in kern else 0
     m = cx.merge(elapsed, n_img, n_img * H * W, n_img * algorithmic_bytes("report", H, W), km, kl)
     del d_imgs
     torch.cuda.empty_cache()
-    res = {"merged": m, "dom": dom, "warm": warm, "warm_steps": nprof, "kern": kern,
-           "stages": {k: stage[j] / args.steps for j, k in enumerate(
+    res = {"merged": m, "dom": dom, "warm": warm, "warm_steps": nprof, "kern": kern, "steps": steps,
+           "stages": {k: stage[j] / steps for j, k in enumerate(
                ("hsv_stats", "fft_rows_cols", "palette_pass2", "gpu_total", "host_total", "host_enqueue",
                 "host_decisions", "host_assembly"))}}
     return res
@@ -760,6 +792,18 @@ def main(argv=None):
             "dominant_kernel": h2["dom"],
             "avg_launch_us_shared_warmup": round(w2.get("avg_us", 0.0), 2)}
     if not args.no_configs:
+        # the same workload on structured images
+        hs = headline(cx, timed_events=False, kind="hblur", steps=max(5, args.steps // 5))
+        ms = hs["merged"]
+        ips = ms["images"] / ms["elapsed"]
+        extra["config2_structured"] = {
+            "workload": f"full report, {args.height}x{args.width} RGB8 structured (synth.py hblur: gradient + disks "
+                        f"+ 15-px horizontal box blur, generated on the device, seed 2 + image index), batch "
+                        f"{args.batch}/GPU, device-resident",
+            "images_per_s": round(ips, 1), "ms_per_step": round(1000 * ms["elapsed"] / hs["steps"], 3),
+            "steps": hs["steps"], "stages_ms_per_step_rank0": hs["stages"],
+            "per_kernel": per_kernel_roofline(hs["warm"], args.batch, args.height, args.width),
+            "roofline_pipeline": pipeline_roofline(ips, args.height, args.width)}
         extra["config4"] = config4(cx, args.config4_images)
         extra["config5"] = config5(cx, args.config5_images)
         if world == 1:
@@ -825,6 +869,8 @@ def main(argv=None):
                                 "launches_timed": int(m["launches"]),
                                 "sampling": "every launch of every 4th timed step, all ranks"}
             line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
+        line["per_kernel"] = per_kernel_roofline(warm, B, H, W)
+        line["roofline_pipeline"] = pipeline_roofline(value, H, W)
         line.update(extra)
         line["vs_baseline_note"] = ("null: BASELINE.md publishes no number for this metric (its only figures are "
                                     "per-stage CPU seconds on an unstated image size, README.md:62-75)")

@@ -206,10 +206,24 @@ int phd_blur_counts(int height, int width, int radius_partitions, int angle_part
  * photohive_dsp_amd/synth.py:uniform (byte j = byte j%8 of word j/8). */
 int phd_fill_uniform_device(uint8_t* d_dst, size_t n, uint64_t seed, void* stream);
 
+/* Fill height x width x 3 bytes of device memory with
+ * photohive_dsp_amd/synth.py:structured(height, width, seed, blur, blur_axis)
+ * (gradient + disks + noise, then a `blur`-tap box blur along blur_axis when
+ * blur > 1): the bench's SURVEY 8(d) row 2(b) images.  0 or -1. */
+int phd_fill_structured_device(uint8_t* d_dst, int height, int width, uint64_t seed, int blur, int blur_axis,
+                               void* stream);
+
 /* Validation hook: per-pixel rgb2hsv and octree group id of n_pixels device
  * RGB8 pixels into d_gid[n] (and d_hsv[3n] if non-NULL). */
 int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, const phd_config* cfg, int* d_gid,
                                 double* d_hsv);
+
+/* Validation hook, host only (no GPU): the production K1's per-pixel
+ * classification (k1_pixel.h) of n interleaved host RGB8 pixels -- the hue
+ * cell of the fused palette, h, s, and (if deferred != NULL) whether the pixel
+ * took the exact double path.  Returns 0 or -1. */
+int phd_debug_k1_pixels(const uint8_t* rgb, long n, const phd_config* cfg, int* cell, double* h, double* s,
+                        int* deferred);
 
 /* Micro-benchmark hook: average ms per launch of one pipeline kernel (0 hsv_stats,
  * 1 fft_rows, 2 fft_cols) over `iters` launches on a device image; `ablate` is a

@@ -270,7 +270,7 @@ static hipError_t cols_impl(const double2* inter, size_t inter_stride, int n, in
                             unsigned long long* bin_sums, double* fmax_part, long out_stride, hipStream_t st) {
     static bool once = (allow_big_lds(k_fft_cols<T, MODE>), true);
     (void)once;
-    static const int ablate = getenv("PHD_ABLATE") ? atoi(getenv("PHD_ABLATE")) : 0;   // debug only
+    static const int ablate = phd_knob("PHD_ABLATE") ? atoi(phd_knob("PHD_ABLATE")) : 0;   // debug only
     phd_launch((k_fft_cols<T, MODE>), dim3((wf + C - 1) / C, n), dim3(T), lds, st, inter, inter_stride, height,
                        wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_part, out_stride, bin_scale(height, wf),
                        ablate);
@@ -286,7 +286,7 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     // columns per block: up to ~3k elements (several blocks per CU; measured
     // on 64-image groups, per launch: 1080 rows C = 2 142 us against C = 8 196,
     // 720 rows C = 4 130 against 171, 512 rows C = 4 54 against 69)
-    static const int cmax = getenv("PHD_FFT_COLS_C") ? atoi(getenv("PHD_FFT_COLS_C")) : 8;   // tuning
+    static const int cmax = phd_knob("PHD_FFT_COLS_C") ? atoi(phd_knob("PHD_FFT_COLS_C")) : 8;   // tuning
     int C = 1;
     while (C < cmax && (size_t)(2 * C) * height <= 3072 && (2 * C) * col_bytes + fixed <= kLdsBudget) C *= 2;
     if (lds_out) *lds_out = C * col_bytes + fixed;

@@ -70,23 +70,27 @@ __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
 }
 
 // One thread's walk over E consecutive rows of a column: p per row in LDS
-// (lgb[r0 + j]), bin ids packed two per word (bmw).  Contiguous rows of one
-// bin form a run whose sum of log p is the log of its product: the frexp
-// mantissas multiply (>= 2^-E, no underflow), the exponents add, and one fp64
-// log closes the run (pgm_normalize_fft's fp64 log, src/fft_processing.c:
+// (lgb[r0 + j]), the column's bin runs in LDS (rl: start row << 16 | bin id,
+// ColRuns), idx = the run holding row r0.  Contiguous rows of one bin form a
+// run whose sum of log p is the log of its product: the frexp mantissas
+// multiply (>= 2^-E, no underflow), the exponents add, and one fp64 log
+// closes the run (pgm_normalize_fft's fp64 log, src/fft_processing.c:
 // 196-199).  Each run adds bin_scale fixed point to its bin with one LDS
 // atomic (order-independent sums).  A thread's first two runs are kept in
 // registers and logged after the walk: a wave then evaluates the fp64 log at
 // most twice (plus the rare third run of a thread), where logging inside the
 // unrolled walk ran it on almost every row (some lane of 64 changes bin there).
 template <int E>
-__device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0, int rend, const unsigned* bmw,
-                                          unsigned long long* bsum, double bscale, const double2* __restrict__ lt) {
+__device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0, int rend, const unsigned* rl,
+                                          int idx, unsigned long long* bsum, double bscale,
+                                          const double2* __restrict__ lt) {
     auto flush = [&](int b, double m, int e) {
         const double acc = fmax((double)e * 0.69314718055994530942 + log_mant(m, lt), 0.0);
         atomicAdd(&bsum[b], bin_fixed(acc, bscale));
     };
-    int cur = -1, esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
+    if (r0 >= rend) return;
+    int cur = (int)(rl[idx] & 0xFFFFu), nxt = (int)(rl[idx + 1] >> 16);   // the sentinel ends every column
+    int esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
     double mprod = 1.0, m0 = 1.0, m1 = 1.0;
     auto close = [&]() {
         if (n == 0) {
@@ -102,10 +106,11 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
         const int r = r0 + j;
         if (r < rend) {
             const double pv = lgb[r];
-            const int bin = (bmw[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
-            if (bin != cur) {
-                if (cur >= 0) close();
-                cur = bin;
+            if (r >= nxt) {                       // the next run starts here (runs are never empty)
+                close();
+                idx++;
+                cur = (int)(rl[idx] & 0xFFFFu);
+                nxt = (int)(rl[idx + 1] >> 16);
                 mprod = 1.0;
                 esum = 0;
             }
@@ -114,7 +119,7 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
             esum += e;
         }
     }
-    if (cur >= 0) close();
+    close();
     if (n > 0) flush(b0, m0, e0);
     if (n > 1) flush(b1, m1, e1);
 }
@@ -320,8 +325,12 @@ struct ColK {
     static constexpr int NT = NC * T;                                     // block size
     static constexpr int CR = (2 * NC * P + NT - 1) / NT;                 // load rounds
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
+    // the run lists of the block's columns (ColRuns): kColRunsMax entries each,
+    // RPT per thread
+    static constexpr int RPT = (kColRunsMax + T - 1) / T;
     static size_t lds(int nbins) {
-        return sizeof(double2) * (NC * H + NTW + kLogTab) + (GB ? 0 : sizeof(unsigned long long) * nbins);
+        return sizeof(double2) * (NC * H + NTW + kLogTab) + sizeof(unsigned) * NC * kColRunsMax +
+               (GB ? 0 : sizeof(unsigned long long) * nbins);
     }
     static_assert(Radices<Rs...>::product == H, "plan");
     // waves per SIMD of the launch bounds: one-column blocks are sized for two
@@ -340,7 +349,8 @@ struct ColK {
 // one-column blocks are sized for two resident blocks per CU
 template <int H, int T, int CPB, int... Rs>
 __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
-                                                     const uint16_t* __restrict__ binmap, int nbins,
+                                                     const unsigned* __restrict__ runs,
+                                                     const uint8_t* __restrict__ segidx, int rstride, int nbins,
                                                      const int* __restrict__ win, int nr,
                                                      unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
                                                      const double2* __restrict__ twg,
@@ -356,7 +366,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     double2* bufs = reinterpret_cast<double2*>(smem);         // [CPB][H]
     double2* tw = bufs + NC * H;
     double2* lt = tw + K::NTW;                                 // log_mant's table
-    unsigned long long* lb = reinterpret_cast<unsigned long long*>(lt + kLogTab);
+    unsigned* rbuf = reinterpret_cast<unsigned*>(lt + kLogTab);          // [NC][kColRunsMax]
+    unsigned long long* lb = reinterpret_cast<unsigned long long*>(rbuf + NC * kColRunsMax);
     const int tid = threadIdx.x;
     // a batch: nimg images of one size, their intermediates, bin sums, max
     // partials and channel sums istride / bstride / fstride / sstride apart;
@@ -462,22 +473,20 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         }
         const int col = 2 * (2 * u + (quad >> 1)) + half;
         const bool live = col < wf;                       // the phantom column of an odd wf idles
-        // bin ids of this thread's run of its column: u in [ht*E, ht*E + E).  The
-        // table has 64 bytes of padding, so the last run may read past its end.
-        unsigned bmw[(K::E + 1) / 2];
+        // the column's bin runs (image-independent, ~0.3 KB per column; ColRuns)
+        // and the run holding this thread's first row ht * E: loaded now, stored
+        // to LDS after the FFT (a phantom column reads column 0's: its p are 1)
+        unsigned rreg[K::RPT];
+        int sidx;
         {
-            const uint16_t* bcol = binmap + (size_t)(live ? col : 0) * H + ht * K::E;
-            if constexpr (K::E % 8 == 0 && (2 * H) % 16 == 0) {
+            const int rc = live ? col : 0;
+            const unsigned* rsrc = runs + (size_t)rc * rstride;
 #pragma unroll
-                for (int j = 0; j < K::E / 8; j++) {
-                    const u32x4 t = reinterpret_cast<const u32x4*>(bcol)[j];
-                    bmw[4 * j] = t.x; bmw[4 * j + 1] = t.y; bmw[4 * j + 2] = t.z; bmw[4 * j + 3] = t.w;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < (K::E + 1) / 2; j++)
-                    bmw[j] = (unsigned)bcol[2 * j] | ((unsigned)bcol[2 * j + 1] << 16);
+            for (int k = 0; k < K::RPT; k++) {
+                const int e = ht + k * T;
+                rreg[k] = e < rstride ? rsrc[e] : 0u;
             }
+            sidx = segidx[(size_t)rc * T + ht];
         }
         if (!K::P0R && K::PF && u + 1 < un && !(ablate & 4)) PHD_COL_FETCH(pair_at(u + 1));
         __syncthreads();
@@ -522,10 +531,14 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         }
         // the next column's pass-0 inputs (p0v is free from here to the next step)
         if (K::P0R && u + 1 < un && !(ablate & 4)) fetch0(pair_at(u + 1));
+        unsigned* rl = rbuf + (NC == 2 ? half * kColRunsMax : 0);   // the previous walk ended at a barrier
+#pragma unroll
+        for (int k = 0; k < K::RPT; k++)
+            if (ht + k * T < kColRunsMax) rl[ht + k * T] = rreg[k];
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
-        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, bmw, bsum, bscale, lt);
+        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, rl, sidx, bsum, bscale, lt);
         __syncthreads();
     }
 #undef PHD_COL_FETCH
@@ -563,7 +576,7 @@ int resident_grid(K kernel, int threads, size_t lds) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess || nb < 1) nb = 1;
     // PHD_FFT_BPC (experiment): at most this many persistent blocks per CU
-    static const int cap = getenv("PHD_FFT_BPC") ? atoi(getenv("PHD_FFT_BPC")) : 0;
+    static const int cap = phd_knob("PHD_FFT_BPC") ? atoi(phd_knob("PHD_FFT_BPC")) : 0;
     if (cap > 0 && nb > cap) nb = cap;
     return nb * num_cus();
 }
@@ -606,7 +619,8 @@ hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, u
                    long sstride = 0) {
     const size_t lds = cols_lds<H, T, CPB, Rs...>(cb.nlb);
     const int grid = cb.grid > 0 ? cb.grid : cols_grid<H, T, CPB, Rs...>(wf, cb.nlb);
-    phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.map, cb.nlb,
+    phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.runs, cb.seg,
+               cb.rstride, cb.nlb,
                cb.win, cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg, istride,
                bstride, fstride, sstride);
     return hipGetLastError();
@@ -670,8 +684,8 @@ hipError_t launch_log_mant(const double* x, double* y, long n, hipStream_t st) {
 }
 
 int ct_variant(bool rows) {
-    static const int vr = getenv("PHD_CT_ROWS_VARIANT") ? atoi(getenv("PHD_CT_ROWS_VARIANT")) : 0;
-    static const int vc = getenv("PHD_CT_COLS_VARIANT") ? atoi(getenv("PHD_CT_COLS_VARIANT")) : 0;
+    static const int vr = phd_knob("PHD_CT_ROWS_VARIANT") ? atoi(phd_knob("PHD_CT_ROWS_VARIANT")) : 0;
+    static const int vc = phd_knob("PHD_CT_COLS_VARIANT") ? atoi(phd_knob("PHD_CT_COLS_VARIANT")) : 0;
     return rows ? vr : vc;
 }
 
@@ -700,6 +714,15 @@ bool ct_cols_plan(int h, std::vector<int>* radices) {
     PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
 #undef PHD_X
     return false;
+}
+
+int fft_cols_ct_threads(int h) {
+    const int n_ = h;
+#define PHD_X(N, V, T, ...) \
+    if (n_ == N && V == v_) return T;
+    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+#undef PHD_X
+    return 0;
 }
 
 size_t fft_cols_ct_lds(int h, int nbins) {

@@ -98,9 +98,8 @@ bool build_blur_table(int height, int width, int nr, int na, BlurTable* t) {
     t->counts.assign((size_t)na * nr, 0);
     for (unsigned i = 0; i < nth; i++)
         for (size_t b = 0; b < t->counts.size(); b++) t->counts[b] += part[i][b];
-    // + kBinMapPad bytes: the FFT column kernels load each thread's run of bin
-    // ids (T threads x ceil(H / T) rows, up to T - 1 rows and a 16-byte load
-    // past the last column's end)
+    // + kBinMapPad bytes: the runtime-plan column kernels may load a run of bin
+    // ids past the last column's end
     if (hipMalloc(&t->d_map, map.size() * sizeof(uint16_t) + kBinMapPad) != hipSuccess) {
         set_error("hipMalloc of the blur bin table failed");
         return false;
@@ -137,26 +136,60 @@ bool build_col_windows(const BlurTable& t, int grid, const std::vector<int>& own
         wmax = std::max(wmax, (a1[b] - a0[b] + 1) * (r1[b] - r0[b] + 1));
     }
     if (wmax > 65535) return false;
-    std::vector<uint16_t> lmap(t.map.size());
+    w->lmap.assign(t.map.size(), 0);
     for (int x = 0; x < wf; x++) {
         const int b = owner[x];
         const uint16_t* col = t.map.data() + (size_t)x * H;
-        uint16_t* lc = lmap.data() + (size_t)x * H;
+        uint16_t* lc = w->lmap.data() + (size_t)x * H;
         for (int u = 0; u < H; u++) {
             const int pb = col[u] / nr, rb = col[u] - pb * nr;
             lc[u] = (uint16_t)((pb - a0[b]) * win[2 * b + 1] + (rb - r0[b]));
         }
     }
-    // + kBinMapPad bytes as d_map (runs past the last column's end)
-    if (hipMalloc(&w->d_lmap, lmap.size() * sizeof(uint16_t) + kBinMapPad) != hipSuccess ||
-        hipMalloc(&w->d_win, win.size() * sizeof(int)) != hipSuccess ||
-        hipMemcpy(w->d_lmap, lmap.data(), lmap.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMalloc(&w->d_win, win.size() * sizeof(int)) != hipSuccess ||
         hipMemcpy(w->d_win, win.data(), win.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
         set_error("upload of the column bin windows failed");
         return false;
     }
     w->grid = grid;
     w->win_max = wmax;
+    return true;
+}
+
+bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r) {
+    const int H = height, E = (H + T - 1) / T;
+    std::vector<int> nrun(wf, 0);
+    int stride = 0;
+    for (int x = 0; x < wf; x++) {
+        const uint16_t* col = map + (size_t)x * H;
+        int n = 1;
+        for (int u = 1; u < H; u++) n += col[u] != col[u - 1];
+        nrun[x] = n;
+        stride = std::max(stride, n + 1);                  // + the sentinel
+    }
+    if (stride > kColRunsMax || H > 65535) return false;
+    std::vector<uint32_t> runs((size_t)wf * stride, (uint32_t)H << 16);
+    std::vector<uint8_t> seg((size_t)wf * T, 0);
+    for (int x = 0; x < wf; x++) {
+        const uint16_t* col = map + (size_t)x * H;
+        uint32_t* rl = runs.data() + (size_t)x * stride;
+        int k = 0;
+        for (int u = 0; u < H; u++) {
+            if (u == 0 || col[u] != col[u - 1]) rl[k++] = ((uint32_t)u << 16) | col[u];
+            // thread t's first row t E lies in run k - 1
+            if (u % E == 0) seg[(size_t)x * T + u / E] = (uint8_t)(k - 1);
+        }
+        rl[k] = (uint32_t)H << 16;                         // sentinel (its bin is never read)
+    }
+    if (hipMalloc(&r->d_runs, runs.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&r->d_seg, seg.size()) != hipSuccess ||
+        hipMemcpy(r->d_runs, runs.data(), runs.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(r->d_seg, seg.data(), seg.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("upload of the column bin runs failed");
+        return false;
+    }
+    r->T = T;
+    r->stride = stride;
     return true;
 }
 

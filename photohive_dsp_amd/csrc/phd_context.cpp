@@ -103,7 +103,7 @@ Context* get_context_lane(int lane) {
 }
 
 unsigned device_event_flags() {
-    static const bool fence = getenv("PHD_EV_FENCE") != nullptr;
+    static const bool fence = phd_knob("PHD_EV_FENCE") != nullptr;
     return fence ? hipEventDisableTiming : hipEventDisableSystemFence;
 }
 
@@ -162,7 +162,7 @@ int lanes_setting() {
 }
 
 int k1_blocks_per_cu() {
-    static const int env = getenv("PHD_K1_BPC") ? std::max(1, std::min(2, atoi(getenv("PHD_K1_BPC")))) : 0;
+    static const int env = phd_knob("PHD_K1_BPC") ? std::max(1, std::min(2, atoi(phd_knob("PHD_K1_BPC")))) : 0;
     return env ? env : (lanes_setting() >= 2 ? 1 : 2);
 }
 
@@ -228,7 +228,7 @@ bool make_fft_plan(int n, FftPlanHost* p, bool composite) {
     P.n = n;
     P.npass = 0;
     int m = n;
-    static const bool small_radices = getenv("PHD_FFT_SMALL_RADICES") != nullptr;   // A/B only
+    static const bool small_radices = phd_knob("PHD_FFT_SMALL_RADICES") != nullptr;   // A/B only
     if (composite && n <= 4096 && !small_radices) {
         // largest radix first: fewer LDS passes (1920 = 16 12 10 in three
         // instead of 8 8 5 3 2 in five)
@@ -329,11 +329,11 @@ const double2* get_ct_twiddles(Context* c, int n, bool rows) {
 // table is the faster, 55.7 against 60.0 us at 4000x3000; 4000-row columns at
 // two blocks per CU instead of one, 103.6 against 143.3 us).
 int col_windows_mode(int set) {
-    static std::atomic<int> mode{getenv("PHD_COL_WINDOWS") ? atoi(getenv("PHD_COL_WINDOWS")) : 1};
+    static std::atomic<int> mode{phd_knob("PHD_COL_WINDOWS") ? atoi(phd_knob("PHD_COL_WINDOWS")) : 1};
     return set >= 0 ? mode.exchange(set) : mode.load();
 }
 
-static const ColWin* get_col_windows(Context* c, const BlurTable& t, int width) {
+static ColWin* get_col_windows(Context* c, const BlurTable& t, int width) {
     const int mode = col_windows_mode(-1);                  // 0 off, 1 where they raise occupancy, 2 always
     if (mode == 0) return nullptr;
     const int nbins = t.na * t.nr;
@@ -343,7 +343,7 @@ static const ColWin* get_col_windows(Context* c, const BlurTable& t, int width) 
     for (int it = 0; it < 3; it++) {
         const auto key = std::make_tuple(t.height, width, t.nr, t.na, grid);
         auto f = c->colwins.find(key);
-        const ColWin* w = nullptr;
+        ColWin* w = nullptr;
         if (f != c->colwins.end()) {
             w = &f->second;
         } else {
@@ -367,22 +367,44 @@ static const ColWin* get_col_windows(Context* c, const BlurTable& t, int width) 
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
                 const BlurTable* tbl, bool batch) {
     *s = FftSel{};
-    static const bool force_generic = getenv("PHD_FFT_GENERIC") != nullptr;   // A/B experiments only
+    static const bool force_generic = phd_knob("PHD_FFT_GENERIC") != nullptr;   // A/B experiments only
     bool ct = !force_generic && ct_rows_plan(width, nullptr) && ct_cols_plan(height, nullptr) &&
               fft_cols_ct_lds(height, nbins) <= 160 * 1024;
     for (int i = 0; ct && i < n; i++)
         if (reinterpret_cast<uintptr_t>(imgs[i]) & 3) ct = false;   // dword row loads
+    // the column pass sums bins from per-column run lists (ColRuns); a table
+    // with more than kColRunsMax runs in a column takes the runtime plans
+    ColWin* w = nullptr;
+    const ColRuns* runs = nullptr;
+    if (ct && tbl) {
+        const int T = fft_cols_ct_threads(height);
+        w = batch ? nullptr : get_col_windows(c, *tbl, width);
+        if (w) {
+            if (w->runs.T == 0 && !build_col_runs(w->lmap.data(), tbl->height, tbl->wf, T, &w->runs)) w = nullptr;
+            else runs = &w->runs;
+        }
+        if (!runs) {
+            const auto key = std::make_tuple(height, width, tbl->nr, tbl->na, T);
+            auto f = c->colruns.find(key);
+            if (f == c->colruns.end()) {
+                ColRuns r;
+                if (build_col_runs(tbl->map.data(), tbl->height, tbl->wf, T, &r)) f = c->colruns.emplace(key, r).first;
+            }
+            if (f != c->colruns.end()) runs = &f->second;
+            else ct = false;
+        }
+    }
     if (ct) {
         s->ct = true;
         s->tw_r = get_ct_twiddles(c, width, true);
         s->tw_c = get_ct_twiddles(c, height, false);
         if (!s->tw_r || !s->tw_c) return false;
-        const ColWin* w = (tbl && !batch) ? get_col_windows(c, *tbl, width) : nullptr;
         if (w) {
-            s->cbins = ColBins{w->d_lmap, w->d_win, w->win_max, tbl->nr, w->grid};
+            s->cbins = ColBins{runs->d_runs, runs->d_seg, runs->stride, w->d_win, w->win_max, tbl->nr, w->grid};
             s->col_blocks = w->grid;
         } else {
-            s->cbins = ColBins{tbl ? tbl->d_map : nullptr, nullptr, nbins, tbl ? tbl->nr : 0, 0};
+            s->cbins = ColBins{runs ? runs->d_runs : nullptr, runs ? runs->d_seg : nullptr, runs ? runs->stride : 0,
+                               nullptr, nbins, tbl ? tbl->nr : 0, 0};
             s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
         }
         return true;
@@ -412,7 +434,7 @@ hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, in
                            const uint16_t* binmap, int nbins, unsigned long long* bin_sums, double* fmax_part,
                            const unsigned long long* sums, double* dbg, hipStream_t st) {
     if (s.ct) {
-        if (!s.cbins.map) return hipErrorInvalidValue;   // select_fft without a table
+        if (!s.cbins.runs) return hipErrorInvalidValue;   // select_fft without a table
         return launch_fft_cols_ct(inter, height, width, wf, s.cbins, bin_sums, fmax_part, s.tw_c, sums, dbg, st);
     }
     if (dbg) return hipErrorNotSupported;

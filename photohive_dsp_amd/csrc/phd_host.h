@@ -71,14 +71,30 @@ struct BlurTable {
     uint16_t* d_map = nullptr;           // device [wf][height]
     int angle_bin_size = 0, radius_bin_size = 0;
 };
+// The compile-time column pass's polar bins as runs (ColBins): along each
+// column the bin id changes a few tens of times (~76 runs per column at
+// 4000x3000, 72 x 40 bins), so a column is its list of runs -- u32 start row
+// << 16 | bin id, then a sentinel whose start is the height -- and each of the
+// kernel's T threads per column gets the index of the run holding its first
+// row (rows [t E, t E + E), E = ceil(height / T)).  ~1.5 MB per size instead
+// of the 12 MB u16 bin of every element.
+struct ColRuns {
+    int T = 0, stride = 0;               // threads per column; entries per column (runs + sentinel)
+    uint32_t* d_runs = nullptr;          // device [wf][stride]
+    uint8_t* d_seg = nullptr;            // device [wf][T]
+};
 // The compile-time column pass's per-block polar-bin windows for one table
 // and grid (ColBins, phd_internal.h): window-local bin ids, each block's first
 // bin and radius width, the largest window.
 struct ColWin {
     int grid = 0, win_max = 0;
-    uint16_t* d_lmap = nullptr;          // device [wf][height]
+    std::vector<uint16_t> lmap;          // host [wf][height] window-local bin ids (the runs are made from it)
     int* d_win = nullptr;                // device [grid][2]
+    ColRuns runs;                        // lmap's runs (T = 0: not built yet)
 };
+// false when a column needs more than kColRunsMax entries (that size then
+// takes the runtime-plan FFT) or on an upload error.
+bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r);
 // Exact (phi_bin, r_bin) of every spectrum element, glibc atan2 + newton_int_sqrt
 // exactly as src/blur_profile.c:87-97 / 427-458.
 bool build_blur_table(int height, int width, int nr, int na, BlurTable* t);
@@ -166,6 +182,7 @@ struct Context {
     std::map<std::pair<int, int>, double2*> ct_tw;  // (length, rows?) -> compile-time plan twiddles
     std::map<std::tuple<int, int, int, int>, BlurTable> tables;
     std::map<std::tuple<int, int, int, int, int>, ColWin> colwins;   // (H, W, nr, na, grid)
+    std::map<std::tuple<int, int, int, int, int>, ColRuns> colruns;  // (H, W, nr, na, T): full-table runs
     std::map<int, GfftPlan> gplans;                 // global-memory FFT plans by length
     double2* d_gbuf = nullptr;                      // generic 2-D path: row pairs + scratch
     size_t gbuf_bytes = 0;

@@ -5,10 +5,25 @@
 #include <hip/hip_runtime_api.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <vector>
 
 namespace phd {
+
+// Experiment switches (PHD_* variables of the timing experiments recorded in
+// alternate schedules, measured-and-rejected kernel forms, ablation
+// masks).  Only the timing build (`make -C photohive_dsp_amd/csrc ablate`,
+// PHD_ABLATE_BUILD) reads them; the production library never looks at the
+// environment for them and always takes the default.
+inline const char* phd_knob(const char* name) {
+#ifdef PHD_ABLATE_BUILD
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
 
 // Events that the next profiled launch records as part of its own dispatch
 // (hipExtLaunchKernel: the kernel's start and end, no event packets between
@@ -171,6 +186,11 @@ int k1t_cshift2(const GridParams& gp, const ClassTables& host_tabs);
 hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int width, const GridParams& gp,
                             const ClassTables* tabs, const PaletteDev& out0, long a_stride, long h_stride,
                             int nchunks, const double* k255, int cshift, int cshift2, hipStream_t st);
+// K1's per-pixel classification (k1_pixel.h) run on the host: hue cell, h, s
+// and whether the pixel took the deferred (exact double) path; -1 when the
+// grid has no code table.
+int k1_host_pixels(const GridParams& gp, const ClassTables& t, const uint8_t* rgb, long n, int* cell, double* h,
+                   double* s, int* deferred);
 // The fused K1's LDS fits this grid (else the palette uses K1 + K3).
 bool fused_palette_ok(const GridParams& gp);
 // Fused palette: the slot sums of the partial (tie-overflow) groups, added
@@ -320,14 +340,20 @@ bool ct_cols_plan(int h, std::vector<int>* radices);
 // `win` when the block adds its window to the image's bins) instead of all
 // na * nr bins: 1.1-14 KB instead of 23 KB of LDS at 72 x 40 bins, which lets
 // two column blocks share a CU where the full table did not fit beside them.
+constexpr int kColRunsMax = 256;   // entries (runs + sentinel) of one column's list (LDS)
 struct ColBins {
-    const uint16_t* map = nullptr;   // [wf][height] bin ids: global (win == nullptr) or window-local
+    const uint32_t* runs = nullptr;  // [wf][rstride] runs of one bin id (ColRuns, phd_host.h): global ids
+                                     // (win == nullptr) or window-local
+    const uint8_t* seg = nullptr;    // [wf][T] the run holding each thread's first row
+    int rstride = 0;                 // entries per column
     const int* win = nullptr;        // [grid][2] {global id of the window's first bin, window radius width}
     int nlb = 0;                     // LDS bins: na * nr, or the largest window
     int nr = 0;                      // radius_partitions (window decode)
     int grid = 0;                    // the grid the windows were made for (0: from occupancy)
 };
 size_t fft_cols_ct_lds(int height, int nlb);
+// threads per column of the compile-time column plan for a height (0: none)
+int fft_cols_ct_threads(int height);
 // log_mant (phd_device.h) over n positive doubles (tests)
 hipError_t launch_log_mant(const double* x, double* y, long n, hipStream_t st);
 // the column-pass bin windows: 0 off, 1 where they raise occupancy (default),
@@ -410,6 +436,8 @@ hipError_t launch_power_bins(const double2* X, int height, int wf, const uint16_
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st);
 hipError_t launch_fill_uniform(uint8_t* dst, size_t n, uint64_t seed, hipStream_t st);
+// synth.py:structured on the device (synth.hip): h x w x 3 bytes
+hipError_t launch_fill_structured(uint8_t* dst, int h, int w, uint64_t seed, int blur, int axis, hipStream_t st);
 // Laplacian-variance sharpness of n crop boxes: sums[2k] = sum f, sums[2k+1] =
 // sum (f - mean)^2 (sums zeroed by the caller).
 hipError_t launch_sharpness(const uint8_t* img, int height, int width, int n, const int* top,

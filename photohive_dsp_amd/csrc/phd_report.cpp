@@ -30,7 +30,7 @@ namespace phd {
 
 // PHD_FFT_OVERLAP=1 (compile-time plans): see run_reports
 static bool overlap_env() {
-    static const bool v = getenv("PHD_FFT_OVERLAP") != nullptr;
+    static const bool v = phd_knob("PHD_FFT_OVERLAP") != nullptr;
     return v;
 }
 
@@ -275,7 +275,7 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
     const double inv_n = 1.0 / (int)n_hsv;
     for (int k = 0; k < np; k++) {
         const double cnt = pal[4 * k + 3];
-        static const bool ablating = getenv("PHD_ABLATE") != nullptr;   // timing experiments only
+        static const bool ablating = phd_knob("PHD_ABLATE") != nullptr;   // timing experiments only
         if (cnt != (double)dec.kept[k] && !ablating) {
             *why = "palette self-check failed: device kept " + std::to_string((long long)cnt) +
                    " pixels for slot " + std::to_string(k) + ", host rules predict " +
@@ -493,9 +493,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // launch per group of images (sizes whose row pairs form whole line groups
     // of the row schedule); small images are otherwise bound by per-launch costs
     const size_t inter_one = sizeof(double2) * ((size_t)(height + 1) * (wf + 1) + 1024);
-    static const bool ctbatch_off = getenv("PHD_CT_NO_BATCH") != nullptr;
+    static const bool ctbatch_off = phd_knob("PHD_CT_NO_BATCH") != nullptr;
     const int q_ct = (int)std::min<size_t>((size_t)n, ((size_t)128 << 20) / inter_one);
-    const bool ct_batchable = !ctbatch_off && !overlap_env() && !getenv("PHD_FFT_PIPE") && n > 1 && q_ct >= 2 &&
+    const bool ct_batchable = !ctbatch_off && !overlap_env() && !phd_knob("PHD_FFT_PIPE") && n > 1 && q_ct >= 2 &&
                               ((height + 1) / 2) % 4 == 0;
     if (!select_fft(c, height, width, nbins, d_imgs, n, &fs, tbl, ct_batchable)) return false;
     const Context::Cls* cls = get_cls(c, gp);
@@ -508,28 +508,28 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // assembly of the early images.  Measured at 4000x3000, 8 images: groups
     // of 1 / 2 / 4 / 8 give FFT stages of 0.857 / 0.838 / 0.828 / 0.823 ms and
     // 6.16k / 6.21k / 6.17k / 6.08k images/s.
-    static const int dl_group = getenv("PHD_DL_GROUP") ? std::max(1, atoi(getenv("PHD_DL_GROUP"))) : 2;
+    static const int dl_group = phd_knob("PHD_DL_GROUP") ? std::max(1, atoi(phd_knob("PHD_DL_GROUP"))) : 2;
     auto dl_end = [&](int i) { return (i + 1) % dl_group == 0 || i == n - 1; };
     auto dl_last = [&](int i) { return std::min(n - 1, (i / dl_group + 1) * dl_group - 1); };
     // fused palette (one pixel pass): ds == 1 and the fused K1's LDS fits; else K1 + K3
-    static const bool two_pass = getenv("PHD_PALETTE_TWO_PASS") != nullptr;
+    static const bool two_pass = phd_knob("PHD_PALETTE_TWO_PASS") != nullptr;
     const bool fused = ds <= 1 && !two_pass && fused_palette_ok(gp);
     const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks, fused ? HueCells::count(gp) : 0);
     // half-spectrum intermediates: one per image of a group of Q (the group's row
     // passes run before its column passes; measured best at Q = 1)
     // (+ 1024 elements of scratch past the tiles for the row pass's dummy stores)
-    static const int qcap = getenv("PHD_FFT_GROUP") ? atoi(getenv("PHD_FFT_GROUP")) : 0;
+    static const int qcap = phd_knob("PHD_FFT_GROUP") ? atoi(phd_knob("PHD_FFT_GROUP")) : 0;
     int Q = std::min(n, qcap > 0 ? qcap : 1);   // 1: the intermediate stays in the 256 MB MALL
     while (Q > 1 && (size_t)Q * inter_one > ((size_t)2 << 30)) Q = (Q + 1) / 2;
     // PHD_FFT_PIPE=1: a two-stream pipeline (rows of image i+1 beside the
     // columns of image i, two intermediates).  Measured slower (5.2k vs 5.8k
     // images/s at 4000x3000: the two 96 MB intermediates no longer share the
     // MALL with the pixels), so the FFTs run serially on one stream by default.
-    static const bool pipe_env = getenv("PHD_FFT_PIPE") != nullptr;
+    static const bool pipe_env = phd_knob("PHD_FFT_PIPE") != nullptr;
     // runtime-plan sizes: the passes of a group of images are one launch each
     // (grid.y = image), the group's intermediates within 128 MB (half the
     // MALL); small images are otherwise bound by per-launch latency
-    static const bool gbatch_off = getenv("PHD_FFT_NO_BATCH") != nullptr;
+    static const bool gbatch_off = phd_knob("PHD_FFT_NO_BATCH") != nullptr;
     const bool gbatch = !fs.ct && !fs.generic && !gbatch_off && n > 1 && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
     if (gbatch) Q = std::max(1, std::min(n, (int)(((size_t)128 << 20) / inter_one)));
     const bool ctbatch = fs.ct && ct_batchable && !fs.cbins.win && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
@@ -557,7 +557,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // dispatch and completion (no marker packets between it and the first row
     // pass), and ev[1] then stands for ev_k1; the A records go down on the
     // download stream, beside the FFTs instead of ahead of them.
-    static const bool k1_events_off = getenv("PHD_K1_MARKERS") != nullptr;
+    static const bool k1_events_off = phd_knob("PHD_K1_MARKERS") != nullptr;
     const bool k1_own = ds <= 1 && !(c->prof.mask & (1u << kK1)) && !k1_events_off &&
                         device_event_flags() == hipEventDisableSystemFence;
     if (k1_own) launch_events() = LaunchEvents{c->ev[0], c->ev[1], false};
@@ -771,7 +771,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         max_slots = std::max(max_slots, h_ns[i]);
     }
     // the second pass on the tail stream, after K1, concurrent with the FFTs
-    static const bool tail_on_fft = getenv("PHD_TAIL_ON_FFT") != nullptr;
+    static const bool tail_on_fft = phd_knob("PHD_TAIL_ON_FFT") != nullptr;
     const hipStream_t s2 = tail_on_fft ? (pipe ? sc : sf) : c->tail;
     PHD_HIP(hipStreamWaitEvent(s2, ev_k1, 0));
     uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
@@ -1456,7 +1456,7 @@ extern "C" int phd_report_batch_u8(const uint8_t* const* images, const int* heig
     std::lock_guard<std::mutex> lk(c->mu);
     if (!upload_init(c)) return -1;
     std::vector<std::vector<int>> groups;
-    static const int gcap = getenv("PHD_HOST_GROUP") ? std::max(1, atoi(getenv("PHD_HOST_GROUP"))) : 16;
+    static const int gcap = phd_knob("PHD_HOST_GROUP") ? std::max(1, atoi(phd_knob("PHD_HOST_GROUP"))) : 16;
     for (auto& g : size_groups(heights, widths, n_images, gcap)) {
         if (precheck(heights[g[0]], widths[g[0]])) groups.push_back(std::move(g));
     }
@@ -1583,6 +1583,23 @@ extern "C" int phd_fill_uniform_device(uint8_t* d_dst, size_t n, uint64_t seed, 
     return 0;
 }
 
+extern "C" int phd_fill_structured_device(uint8_t* d_dst, int height, int width, uint64_t seed, int blur,
+                                          int blur_axis, void* stream) {
+    clear_error();
+    Context* c = get_context();
+    if (!c || !d_dst || height < 1 || width < 1 || blur < 0 || (blur_axis != 0 && blur_axis != 1)) return -1;
+    hipStream_t st = work_stream(c, stream);
+    if (launch_fill_structured(d_dst, height, width, seed, blur, blur_axis, st) != hipSuccess) {
+        set_error("structured fill kernel launch failed");
+        return -1;
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        set_error("structured fill kernel failed");
+        return -1;
+    }
+    return 0;
+}
+
 extern "C" int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, const phd_config* cfg, int* d_gid,
                                            double* d_hsv) {
     clear_error();
@@ -1600,6 +1617,29 @@ extern "C" int phd_debug_hsv_groups_device(const uint8_t* d_rgb, long n_pixels, 
     if (launch_debug_hsv(d_rgb, n_pixels, gp, cls->fc, cls->d, c->d_k255, d_gid, d_hsv, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         set_error("debug hsv kernel failed");
+        return -1;
+    }
+    return 0;
+}
+
+// K1's per-pixel logic on the host, no GPU (tests/test_k1_pixel.py): for n
+// interleaved RGB8 pixels the hue cell (HueCells layout), h, s and the
+// deferred flag exactly as k1.hip classifies them.
+extern "C" int phd_debug_k1_pixels(const uint8_t* rgb, long n, const phd_config* cfg, int* cell, double* h,
+                                   double* s, int* deferred) {
+    clear_error();
+    if (!rgb || !cfg || !cell || !h || !s || n < 0) return -1;
+    std::string why;
+    if (!validate_config(*cfg, &why)) {
+        set_error(why);
+        return -1;
+    }
+    const GridParams gp = make_grid(*cfg);
+    FastCls fc;
+    std::unique_ptr<ClassTables> t(new ClassTables());
+    make_class_tables(gp, &fc, t.get());
+    if (k1_host_pixels(gp, *t, rgb, n, cell, h, s, deferred) != 0) {
+        set_error("phd_debug_k1_pixels: this grid has no K1 code table");
         return -1;
     }
     return 0;
@@ -1641,7 +1681,7 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
     pd.s_part = (double*)(dw + 256 + 4 * 4096);
     pd.chunk_hist = (unsigned short*)(dw + 256 + 4 * 4096 + 8 * (size_t)nchunks);
     // K1 is timed as the report runs it: fused when the report fuses
-    const bool fused = ds <= 1 && getenv("PHD_PALETTE_TWO_PASS") == nullptr && fused_palette_ok(gp);
+    const bool fused = ds <= 1 && phd_knob("PHD_PALETTE_TWO_PASS") == nullptr && fused_palette_ok(gp);
     void* fscratch = nullptr;
     if (fused) {
         if (hipMalloc(&fscratch, sizeof(double) * 3 * gp.tl + sizeof(unsigned) * HueCells::count(gp)) != hipSuccess)

@@ -46,7 +46,7 @@ HostPool* copy_pool() {
 }
 
 static bool staged_upload() {
-    static const bool staged = getenv("PHD_UPLOAD") && !strcmp(getenv("PHD_UPLOAD"), "staged");
+    static const bool staged = phd_knob("PHD_UPLOAD") && !strcmp(phd_knob("PHD_UPLOAD"), "staged");
     return staged;
 }
 
@@ -107,7 +107,7 @@ static bool staged_init(Context* c, std::string* why) {
 // buffer is no longer read); the DMA may still be running.
 
 int upload_streams() {
-    static const int n = getenv("PHD_UPLOAD_STREAMS") ? std::min(2, std::max(1, atoi(getenv("PHD_UPLOAD_STREAMS"))))
+    static const int n = phd_knob("PHD_UPLOAD_STREAMS") ? std::min(2, std::max(1, atoi(phd_knob("PHD_UPLOAD_STREAMS"))))
                                                       : 1;
     return staged_upload() ? 1 : n;
 }

@@ -291,11 +291,11 @@ hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     const long nitems = (long)n * nchunks;
     // non-temporal loads (the pixels are streamed once): 0.74 of the HBM peak
     // against 0.70-0.72 with plain loads (PHD_STATS_PLAIN=1)
-    static const bool nt = getenv("PHD_STATS_PLAIN") == nullptr;
+    static const bool nt = phd_knob("PHD_STATS_PLAIN") == nullptr;
     // PHD_STATS_MODE (config 3, 512 x 1080p, fraction of the 8 TB/s peak):
     // 3 (default) exact sum of d per max value; 0 fp32 pair sums 0.71-0.74 (round
     // 2); 1 + the 0.999999 count 0.60-0.63; 2 + compensated quotients 0.57
-    static const int mode = getenv("PHD_STATS_MODE") ? atoi(getenv("PHD_STATS_MODE")) : 3;
+    static const int mode = phd_knob("PHD_STATS_MODE") ? atoi(phd_knob("PHD_STATS_MODE")) : 3;
 #define PHD_ST(NT, M)                                                                                          \
     do {                                                                                                       \
         /* the persistent grid is sized for the variant launched */                                            \

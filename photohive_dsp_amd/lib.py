@@ -76,9 +76,15 @@ lib.phd_blur_counts.restype = ctypes.c_int
 lib.phd_blur_counts.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P(ctypes.c_longlong)]
 lib.phd_fill_uniform_device.restype = ctypes.c_int
 lib.phd_fill_uniform_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]
+lib.phd_fill_structured_device.restype = ctypes.c_int
+lib.phd_fill_structured_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p]
 lib.phd_debug_hsv_groups_device.restype = ctypes.c_int
 lib.phd_debug_hsv_groups_device.argtypes = [ctypes.c_void_p, ctypes.c_long, P(PhdConfig), ctypes.c_void_p,
                                             ctypes.c_void_p]
+lib.phd_debug_k1_pixels.restype = ctypes.c_int
+lib.phd_debug_k1_pixels.argtypes = [ctypes.c_void_p, ctypes.c_long, P(PhdConfig), ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]
 lib.phd_profile_kernels.restype = ctypes.c_int
 lib.phd_profile_kernels.argtypes = [ctypes.c_uint]
 lib.phd_profile_read.restype = ctypes.c_int

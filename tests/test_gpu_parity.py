@@ -385,7 +385,9 @@ def test_device_synthetic_fill_matches_numpy():
     np.testing.assert_array_equal(t.cpu().numpy(), synth.uniform(401, 577, 7).ravel())
 
 
-@pytest.mark.parametrize("kind,seed", [("uniform", 1), ("structured", 2), ("dominant", 3)])
+@pytest.mark.parametrize("kind,seed", [("uniform", 1), ("structured", 2), ("dominant", 3),
+                                       # gradient + disks + 15-px horizontal box blur
+                                       ("hblur", 2)])
 def test_full_size_4000x3000_against_oracle(kind, seed):
     """BASELINE config 2 size: the whole report against the CPU oracle."""
     phd, L, _ = _phd()

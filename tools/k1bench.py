@@ -38,7 +38,7 @@ for n, h, w in [(64, 1080, 1920), (512, 1080, 1920)]:
     us = k1_avg()
     print(f"[{tag}] hsv_stats {n}x{h}x{w}: {us:.1f} us/launch  {n * h * w * 3 / us / 1e3:.0f} GB/s")
     del t
-n, h, w = 8, 3000, 4000
+n, h, w = int(os.environ.get("K1N", "64")), 3000, 4000
 t = fill(n, h, w)
 cfg = make_config()
 outs = (ctypes.POINTER(Full_Report_Data) * n)()
