@@ -22,11 +22,14 @@ ABL = os.path.join(ROOT, "photohive_dsp_amd", "PhotoHive_DSP_lib", "libreport_da
 H, W = 3000, 4000
 WF = W // 2 + 1
 KNOWN = {  # algorithmic read bytes per launch
-    "k_cols_ct": 16 * H * (WF + 1) + 2 * H * WF,      # tiles (phantom column included) + u16 bin map
+    "k_cols_ct": 16 * H * (WF + 1),                     # tiles (phantom column included); the bin runs are ~1.5 MB
     "k_rows_ct": 3 * H * W,                             # RGB8
+    "k_rgb_stats": 8 * 3 * H * W,                       # RGB8 of tools/stats_bench.py's 8-image launches
 }
 RUNS = [("k_cols_ct", 2, 0, False), ("k_cols_ct", 2, 1 | 2 | 16, True),
-        ("k_rows_ct", 1, 0, False), ("k_rows_ct", 1, 1 | 2, True)]
+        ("k_rows_ct", 1, 0, False), ("k_rows_ct", 1, 1 | 2, True),
+        # K1's per-lane dwordx3 pattern: the statistics pass reads each byte once
+        ("k_rgb_stats", -1, 0, False)]
 
 
 def fetch(kernel_id, mask, ablate_lib, tag):
@@ -34,8 +37,10 @@ def fetch(kernel_id, mask, ablate_lib, tag):
     env = dict(os.environ)
     if ablate_lib:
         env["PHD_LIB"] = ABL
+    prog = ([os.path.join(ROOT, "tools", "stats_bench.py")] if kernel_id < 0 else
+            [os.path.join(ROOT, "tools", "kbench.py"), str(kernel_id), str(mask)])
     cmd = ["rocprofv3", "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "p", "--",
-           sys.executable, os.path.join(ROOT, "tools", "kbench.py"), str(kernel_id), str(mask)]
+           sys.executable] + prog
     subprocess.run(cmd, cwd=ROOT, env=env, check=True, timeout=150)
     f = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)[0]
     vals = {}
@@ -58,6 +63,12 @@ def main():
         res["runs"][f"{k} ablate {mask}"] = {"fetch_size_kb": avg, "launches": len(kb),
                                              "fetch_bytes_x1024": avg * 1024}
     for k in KNOWN:
+        if k == "k_rgb_stats":
+            moved = res["runs"].get(f"{k} ablate 0", {}).get("fetch_bytes_x1024")
+            if moved:
+                # applied to K1 (k_k1t), whose loads are the same 12-byte-per-lane pattern
+                res[k] = {"factor": KNOWN[k] / moved, "applies_to": "k_k1t"}
+            continue
         moved = res["runs"].get(f"{k} ablate {1 | 2 | 16 if k == 'k_cols_ct' else 1 | 2}", {}).get("fetch_bytes_x1024")
         prod = res["runs"].get(f"{k} ablate 0", {}).get("fetch_bytes_x1024")
         if moved and prod:

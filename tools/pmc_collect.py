@@ -75,7 +75,7 @@ def main():
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_calib.json")) as f:
             cal = json.load(f)
-        for kname, short_name in (("k_cols_ct", "fft_cols"), ("k_rows_ct", "fft_rows")):
+        for kname, short_name in (("k_cols_ct", "fft_cols"), ("k_rows_ct", "fft_rows"), ("k_rgb_stats", "hsv_stats")):
             if kname in cal and cal.get("image") == f"{a.height}x{a.width}":
                 factors[short_name] = cal[kname]["factor"]
         if factors:
