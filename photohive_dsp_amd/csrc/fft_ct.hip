@@ -10,9 +10,11 @@
 //
 // Intermediate layout (half spectrum after the row pass), tiled so that both
 // passes move whole 64-byte pieces: element (y, k) of row pair p = y/2 and
-// column pair kp = k/2 sits at ((p * KP + kp) * 2 + k%2) * 2 + y%2, with
-// KP = ceil((W/2+1) / 2).  A row pair's spectrum is one contiguous 64 KB run
-// (W = 4000); a column pair is 1500 pieces of 64 B (H = 3000).
+// column pair kp = k/2 sits at p * RS + (kp * 2 + k%2) * 2 + y%2, with
+// KP = ceil((W/2+1) / 2) and RS = ct_row_stride(W), 4 KP rounded up to 8
+// elements so each row pair starts on a 128-byte line.  A row pair's spectrum
+// is one contiguous 64 KB run (W = 4000); a column pair is 1500 pieces of 64 B
+// (H = 3000).
 //
 // Row kernel (persistent, 2 blocks per CU).  Each step handles one pair of
 // image rows.  Both rows' RGB8 bytes were prefetched into registers (dwordx3 =
@@ -89,7 +91,13 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
         atomicAdd(&bsum[b], bin_fixed(acc, bscale));
     };
     if (r0 >= rend) return;
-    int cur = (int)(rl[idx] & 0xFFFFu), nxt = (int)(rl[idx + 1] >> 16);   // the sentinel ends every column
+    // the thread's first four entries in registers (one LDS latency), refilled
+    // one entry per run change; entries past the column's sentinel are never
+    // used (the sentinel's start is the height)
+    const unsigned q0 = rl[idx];
+    unsigned q1 = rl[idx + 1], q2 = rl[min(idx + 2, kColRunsMax - 1)], q3 = rl[min(idx + 3, kColRunsMax - 1)];
+    int qi = idx + 4;
+    int cur = (int)(q0 & 0xFFFFu), nxt = (int)(q1 >> 16);
     int esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
     double mprod = 1.0, m0 = 1.0, m1 = 1.0;
     auto close = [&]() {
@@ -108,9 +116,11 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
             const double pv = lgb[r];
             if (r >= nxt) {                       // the next run starts here (runs are never empty)
                 close();
-                idx++;
-                cur = (int)(rl[idx] & 0xFFFFu);
-                nxt = (int)(rl[idx + 1] >> 16);
+                cur = (int)(q1 & 0xFFFFu);
+                q1 = q2;
+                q2 = q3;
+                q3 = rl[min(qi++, kColRunsMax - 1)];
+                nxt = (int)(q1 >> 16);
                 mprod = 1.0;
                 esum = 0;
             }
@@ -210,8 +220,8 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     // the prefetched pixels counts the stores instead of draining them.
     constexpr int WF_ = W / 2 + 1, KP_ = (WF_ + 1) / 2, NSO_ = (4 * KP_ + T - 1) / T;
     {
-        // a scratch run just past the tiles (the intermediate has (H+1)(W/2+2) elements)
-        double2* slot = inter + (size_t)P * KP_ * 4 + (blockIdx.x & 63) * NSO_;
+        // a scratch run just past the tiles (inter_elems: 1024 elements of slack)
+        double2* slot = inter + (size_t)P * ct_row_stride(W) + (blockIdx.x & 63) * NSO_;
 #pragma unroll
         for (int j = 0; j < NSO_; j++)
             if ((4 * KP_) % T == 0 || tid + j * T < 4 * KP_) slot[j] = make_double2(0.0, 0.0);
@@ -256,11 +266,12 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
         __syncthreads();
         if (!(ablate & 1)) fft_lds<W, T, 1, Rs...>(buf, tw, tid);
         constexpr int WF = W / 2 + 1, KP = (WF + 1) / 2;
-        // the pair's tile row, contiguous: thread i -> (column pair i/4, column
-        // k = 2(i/4) + (i/2)%2, row y0 + i%2); the phantom column WF (odd WF) is 0
-        // (a fixed, unrolled count per thread, branch-free: the next step's wait
-        // for its prefetched pixels can then count these stores exactly)
-        double2* orow = inter + im * istride + (size_t)pr * KP * 4;
+        // the pair's tile row, contiguous and 128-byte aligned (ct_row_stride):
+        // thread i -> (column pair i/4, column k = 2(i/4) + (i/2)%2, row y0 +
+        // i%2); the phantom column WF (odd WF) is 0 (a fixed, unrolled count per
+        // thread, branch-free: the next step's wait for its prefetched pixels can
+        // then count these stores exactly)
+        double2* orow = inter + im * istride + (size_t)pr * ct_row_stride(W);
         constexpr int NSO = (4 * KP + T - 1) / T;
 #pragma unroll
         for (int j = 0; j < NSO; j++) {
@@ -389,6 +400,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     log_table_init(lt, tid, NT);
     unsigned long long* bsum = K::GB ? bin_sums : lb;         // where the runs are added
     const int kpn = (wf + 1) / 2;
+    const size_t rs = (size_t)((4 * kpn + 7) & ~7);           // row-pair stride (ct_row_stride)
     const int nunit = (kpn + 1) / 2;                          // tile pairs (128-byte lines)
     const int nlog = NC == 2 ? (int)gridDim.x / 2 : (int)gridDim.x / 4;
     const int lblk = NC == 2 ? (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7))
@@ -411,11 +423,11 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
 #define PHD_COL_FETCH(kpv)                                                                  \
     do {                                                                                    \
         const u32x4* src_ = reinterpret_cast<const u32x4*>(inter) +                         \
-                            ((size_t)prow0 * kpn + (kpv)) * 4 + psub;                       \
+                            (size_t)prow0 * rs + (size_t)(kpv) * 4 + psub;                  \
         _Pragma("unroll") for (int c = 0; c < K::CR; c++) {                                \
             /* rows past the end re-read the last row pair (unused, no branch) */           \
             const int pr_ = min(c * (NT / PER), K::P - 1 - prow0);                          \
-            pf[c] = src_[(size_t)pr_ * kpn * 4];                                            \
+            pf[c] = src_[(size_t)pr_ * rs];                                                 \
         }                                                                                   \
     } while (0)
     // K::P0R: thread ht < NB0 holds rows ht + r NB0 of its column (pass 0's inputs)
@@ -427,7 +439,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
 #pragma unroll
             for (int r = 0; r < (K::P0R ? R0 : 1); r++) {
                 const int y = ht + r * NB0;
-                p0v[0][r] = src[(size_t)(y >> 1) * kpn * 4 + (y & 1)];
+                p0v[0][r] = src[(size_t)(y >> 1) * rs + (y & 1)];
             }
         }
     };

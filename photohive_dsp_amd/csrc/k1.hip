@@ -61,14 +61,15 @@ constexpr int kCellBytes = 24;   // {u64 count word, f64 sum h, f64 sum s}
 
 // LDS carve (bytes).
 struct LVar {
-    int cells, code, k255, red, rcell, cg, seg, r255, rmx, gacc, end;
+    int cells, code, k255, inv, red, rcell, cg, seg, r255, rmx, gacc, end;
 };
-__host__ __device__ inline LVar l_var(int tl, int ncell, int cshift, int code_bytes) {
+__host__ __device__ inline LVar l_var(int tl, int ncell, int cshift, int code_bytes, bool k255 = true) {
     LVar v;
     v.cells = 0;                                                    // (ncell + 1) << cshift cells
     v.code = (kCellBytes * ((ncell + 1) << cshift) + 15) & ~15;     // code_bytes u8
     v.k255 = (v.code + code_bytes + 15) & ~15;                      // 256 f64: k / 255.0 (deferred pixels)
-    v.red = v.k255 + 2048;                                          // 16 waves x 8 u64
+    v.inv = v.k255 + (k255 ? 2048 : 0);                             // 256 K1Inv (16 B)
+    v.red = v.inv + 256 * (int)sizeof(K1Inv);                       // 16 waves x 8 u64
     v.rcell = v.red + 1024;                                         // ncell u32: the run's cell counts
     v.cg = v.rcell + 4 * ncell;                                     // tl u32: the chunk's group counts
     v.seg = v.cg + 4 * tl;                                          // tl u32: the run's group counts
@@ -104,6 +105,7 @@ struct Mom {
 template <bool TRI, bool SMALL>
 __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
                                              const unsigned char* __restrict__ code8,
+                                             const K1Inv* __restrict__ inv,
                                              unsigned char* __restrict__ cells, int cshift, int copy,
                                              const K1Grid& G) {
     const u16x2 one = {1, 1};
@@ -140,21 +142,30 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
         const int q = i & 1, sh = 16 * (i >> 1);           // pixel i: pair q, half i >> 1
         code[i] = code8[code_idx<TRI>((Mx[q] >> sh) & 0xFFFF, (Kd[q] >> sh) & 0xFFFF)];
     }
+    K1Inv ekd[4];
+    double ikm[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int q = i & 1, sh = 16 * (i >> 1);
+        const int kmx = (Mx[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
+        ekd[i] = inv[kd > 1 ? kd : 1];
+        ikm[i] = inv[kmx > 1 ? kmx : 1].inv;
+    }
     unsigned def = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);
         const int kr = (R[q] >> sh) & 0xFFFF, kg = (Gc[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
-        const K1Px p = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kd, code[i], G);
+        const K1Px p = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kd, code[i], ekd[i], ikm[i], G);
         cell_add(cells, p.cell, cshift, copy, p);
         def |= (unsigned)(p.cell == G.ncell) << i;
     }
     return def;
 }
 
-template <int KT, bool TRI, bool SMALL>
-__global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict__ imgs, long npix, int nchunks,
+template <int KT, bool TRI, bool SMALL, int MINW = 4, bool LEAN = false>
+__global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restrict__ imgs, long npix, int nchunks,
                                                long nitems, GridParams gp, K1Grid G,
                                                const ClassTables* __restrict__ tabs,
                                                const double* __restrict__ k255g, PaletteDev out, long a_stride,
@@ -167,10 +178,12 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
     constexpr int kT = KT, kG = kChunk / (4 * KT);              // threads; 4-pixel groups per thread per chunk
     static_assert(kG == 4 || kG == 8, "K1 tile");
     const int tl = gp.tl, ncell = G.ncell;
-    const LVar V = l_var(tl, ncell, cshift, code_bytes<TRI>());
+    const LVar V = l_var(tl, ncell, cshift, code_bytes<TRI>(), MINW <= 4);
     unsigned char* cells = smem + V.cells;
     unsigned char* code8 = smem + V.code;
-    double* k255 = reinterpret_cast<double*>(smem + V.k255);
+    K1Inv* inv = reinterpret_cast<K1Inv*>(smem + V.inv);
+    // the three-block form (MINW 6) has no LDS k / 255 table: k1_exact divides
+    double* k255 = MINW > 4 ? nullptr : reinterpret_cast<double*>(smem + V.k255);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + V.red);
     unsigned* rcell = reinterpret_cast<unsigned*>(smem + V.rcell);
     unsigned* cg = reinterpret_cast<unsigned*>(smem + V.cg);
@@ -183,7 +196,10 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         const uint4* src = reinterpret_cast<const uint4*>(TRI ? tabs->code_tri : tabs->code8);
         uint4* dst = reinterpret_cast<uint4*>(code8);
         for (int i = tid; i < code_bytes<TRI>() / 16; i += kT) dst[i] = src[i];
-        for (int i = tid; i < 256; i += kT) k255[i] = k255g[i];
+        if (k255)
+            for (int i = tid; i < 256; i += kT) k255[i] = k255g[i];
+        for (int k = tid; k < 256; k += kT)        // as k1_inv_init: correctly rounded quotients
+            inv[k] = k ? K1Inv{1.0 / (double)k, 1.0f / (float)k, 0u} : K1Inv{0.0, 0.0f, 0u};
         unsigned* z = reinterpret_cast<unsigned*>(smem);
         for (int i = tid; i < V.code / 4; i += kT) z[i] = 0u;                        // cells
         for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;           // run records
@@ -222,18 +238,20 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             }
         }
     };
-    issue(ip, c);
+    if (!LEAN) issue(ip, c);
     Mom m{0, 0, 0, 0, 0, 0};
     int seg_c0 = c;
     long seg_it0 = it0;
     for (long it = it0; it < it1; it++) {
         const long base = (long)c * kChunk;
         unsigned cw[kG][3];
+        if (!LEAN) {
 #pragma unroll
-        for (int st = 0; st < kG; st++) {
-            cw[st][0] = w[st][0];
-            cw[st][1] = w[st][1];
-            cw[st][2] = w[st][2];
+            for (int st = 0; st < kG; st++) {
+                cw[st][0] = w[st][0];
+                cw[st][1] = w[st][1];
+                cw[st][2] = w[st][2];
+            }
         }
         const int cimg = img, cc = c;
         if (++c == nchunks) {
@@ -243,14 +261,38 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         const bool more = it + 1 < it1;
         if (more) {
             if (img != cimg) ip = imgs[img];
-            issue(ip, c);
+            if (!LEAN) issue(ip, c);
         }
         const uint8_t* cip = imgs[cimg];
         unsigned emask = 0;                                       // deferred pixels (bit 4 st + i)
+        if constexpr (LEAN) {
+            // one group (4 pixels) ahead only and the group loop not unrolled:
+            // ~100 VGPRs without spills where the whole next chunk in registers
+            // took 128 and spilled; the other waves of the CU hide the loads
+            auto ld = [&](int st, unsigned& x0, unsigned& x1, unsigned& x2) {
+                const bool ok = base + 4L * tid + 4L * kT * st < full_end;
+                gu32t* q = (gu32t*)(cip + (ok ? (unsigned)(3 * (base + 4L * tid)) + 12u * kT * st : 0u));
+                x0 = ok ? q[0] : 0u;
+                x1 = ok ? q[1] : 0u;
+                x2 = ok ? q[2] : 0u;
+            };
+            unsigned a0, a1, a2;
+            ld(0, a0, a1, a2);
+#pragma unroll 1
+            for (int st = 0; st < kG; st++) {
+                unsigned n0 = 0, n1 = 0, n2 = 0;
+                if (st + 1 < kG) ld(st + 1, n0, n1, n2);
+                emask |= k1_group<TRI, SMALL>(a0, a1, a2, m, code8, inv, cells, cshift, copy, G) << (4 * st);
+                a0 = n0;
+                a1 = n1;
+                a2 = n2;
+            }
+        } else {
 #pragma unroll
-        for (int st = 0; st < kG; st++)
-            emask |= k1_group<TRI, SMALL>(cw[st][0], cw[st][1], cw[st][2], m, code8, cells, cshift, copy, G)
-                     << (4 * st);
+            for (int st = 0; st < kG; st++)
+                emask |= k1_group<TRI, SMALL>(cw[st][0], cw[st][1], cw[st][2], m, code8, inv, cells, cshift, copy, G)
+                         << (4 * st);
+        }
         const bool last_chunk = base + kChunk >= npix;            // block-uniform
         if (last_chunk && tid == 0) {
             // the < 4 pixels of a partial final group
@@ -260,7 +302,8 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                 m.qr += kr * kr; m.qg += kg * kg; m.qb += kb * kb;
                 const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
                 const int code = code8[code_idx<TRI>(kmx, kmx - kmn)];
-                K1Px px = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kmx - kmn, code, G);
+                K1Px px = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kmx - kmn, code, inv[kmx - kmn > 1 ? kmx - kmn : 1],
+                                          inv[kmx > 1 ? kmx : 1].inv, G);
                 if (px.cell == ncell) px = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
                 cell_add(cells, px.cell, cshift, copy, px);
             }
@@ -387,20 +430,21 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
     }
 }
 
-template <int KT, bool TRI>
+template <int KT, bool TRI, int MINW = 4, bool LEAN = false>
 void launch_form(int grid, size_t lds, hipStream_t st, const uint8_t* const* d_imgs, long npix, int nchunks,
                  long nitems, const GridParams& gp, const K1Grid& G, const ClassTables* tabs, const double* k255,
                  const PaletteDev& out0, long a_stride, long h_stride, int cshift) {
     if (G.small_c)
-        phd_launch((k_k1t<KT, TRI, true>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
-                   k255, out0, a_stride, h_stride, cshift);
+        phd_launch((k_k1t<KT, TRI, true, MINW, LEAN>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
+                   gp, G, tabs, k255, out0, a_stride, h_stride, cshift);
     else
-        phd_launch((k_k1t<KT, TRI, false>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems, gp, G,
-                   tabs, k255, out0, a_stride, h_stride, cshift);
+        phd_launch((k_k1t<KT, TRI, false, MINW, LEAN>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
+                   gp, G, tabs, k255, out0, a_stride, h_stride, cshift);
 }
 
 constexpr int kLds1 = 158 * 1024;   // one block per CU
 constexpr int kLds2 = 79 * 1024;    // two blocks per CU
+constexpr int kLds3 = 160 * 1024 / 3 - 256;   // three blocks per CU
 
 }  // namespace
 
@@ -434,7 +478,9 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     static const bool attr = [] {
         const void* fs[] = {(const void*)k_k1t<1024, false, true>, (const void*)k_k1t<1024, false, false>,
                             (const void*)k_k1t<1024, true, true>,  (const void*)k_k1t<1024, true, false>,
-                            (const void*)k_k1t<512, true, true>,   (const void*)k_k1t<512, true, false>};
+                            (const void*)k_k1t<512, true, true>,   (const void*)k_k1t<512, true, false>,
+                            (const void*)k_k1t<512, true, true, 6, true>, (const void*)k_k1t<512, true, false, 6, true>,
+                            (const void*)k_k1t<512, true, true, 4, true>, (const void*)k_k1t<512, true, false, 4, true>};
         for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -443,6 +489,26 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     // (half a CU each): it wins when it has at least ~2 chunks per block, not
     // for a single image's 732 chunks where its last chunks form the tail
     const long cus = num_cus();
+    // timing experiments (PHD_K1_FORM): 3 = three 512-thread blocks per CU, one
+    // lane copy of the cells, no k / 255 table (53 KiB each), 6 waves per SIMD
+    // (measured slower: 44.9 against 40.9 us per image before the reciprocal
+    // table); 5 = the two-block form with the whole next chunk prefetched into
+    // registers (the round-3 loop: 128 VGPRs, spills)
+    static const int form = phd_knob("PHD_K1_FORM") ? atoi(phd_knob("PHD_K1_FORM")) : 0;
+    const size_t lds3 = (size_t)l_var(gp.tl, ncell, 0, code_bytes<true>(), false).end;
+    if (form == 3 && cshift2 >= 0 && lds3 <= (size_t)kLds3) {
+        const int grid = (int)std::min<long>(nitems, 3 * cus);
+        launch_form<512, true, 6, true>(grid, lds3, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
+                                        a_stride, h_stride, 0);
+        return hipGetLastError();
+    }
+    if (form == 5 && cshift2 >= 0) {
+        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
+        const int grid = (int)std::min<long>(nitems, 2 * cus);
+        launch_form<512, true, 4, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
+                                         a_stride, h_stride, cshift2);
+        return hipGetLastError();
+    }
     const bool two = cshift2 >= 0 &&
                      (cshift < 0 || 19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus));
     if (two) {                                            // two 512-thread blocks per CU
@@ -450,8 +516,8 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
         // with two lanes, one block per CU: the other half of each CU stays free
         // for the other lane's FFT blocks (k1_blocks_per_cu)
         const int grid = (int)std::min<long>(nitems, (long)k1_blocks_per_cu() * cus);
-        launch_form<512, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0, a_stride,
-                               h_stride, cshift2);
+        launch_form<512, true, 4, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
+                                        a_stride, h_stride, cshift2);
     } else {                                              // one 1024-thread block per CU
         const int grid = (int)std::min<long>(nitems, cus);
         // the triangular code table leaves 31 KiB more for lane copies of the
@@ -482,12 +548,16 @@ int k1_host_pixels(const GridParams& gp, const ClassTables& t, const uint8_t* rg
     k1_grid_init(G, gp);
     double k255[256];
     for (int k = 0; k < 256; k++) k255[k] = (double)k / 255.0;
+    K1Inv inv[256];
+    k1_inv_init(inv);
     for (long i = 0; i < n; i++) {
         const int kr = rgb[3 * i], kg = rgb[3 * i + 1], kb = rgb[3 * i + 2];
         const int kmx = std::max(kr, std::max(kg, kb)), kmn = std::min(kr, std::min(kg, kb)), kd = kmx - kmn;
         const int code = t.code8[kmx * 256 + kd];
-        K1Px p = G.small_c ? k1_pixel<true>(kr, kg, kb, kmx, kmn, kd, code, G)
-                           : k1_pixel<false>(kr, kg, kb, kmx, kmn, kd, code, G);
+        const K1Inv& ekd = inv[kd > 1 ? kd : 1];
+        const double ikm = inv[kmx > 1 ? kmx : 1].inv;
+        K1Px p = G.small_c ? k1_pixel<true>(kr, kg, kb, kmx, kmn, kd, code, ekd, ikm, G)
+                           : k1_pixel<false>(kr, kg, kb, kmx, kmn, kd, code, ekd, ikm, G);
         const bool def = p.cell == G.ncell;
         if (def) p = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
         cell[i] = p.cell;

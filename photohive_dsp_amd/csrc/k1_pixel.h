@@ -39,6 +39,7 @@ namespace phd {
 // Grid constants of one launch (uniform).
 struct K1Grid {
     int lh;          // Lh = 360 / h_partitions (integer, color_quantization.c:41)
+    float rlh;       // 1 / Lh in fp32 (k1_halfbin)
     int hp, hp2;     // h_partitions, 2 h_partitions
     int spvp;        // colour codes: 0 .. spvp - 1
     int ac;          // 4 spvp - 2: cell step per hue bin of a colour code
@@ -60,25 +61,23 @@ K1_HD int k1_mul(int a, int b) {
 #endif
 }
 
-K1_HD float k1_rcpf(float x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_rcpf(x);
-#else
-    return 1.0f / x;
-#endif
-}
-
-// a / b for integers 0 <= a < 2^24, 1 <= b <= 255 in fp64 to ~2^-45 relative:
-// an fp32 reciprocal refined by one Newton step in fp64 (the residual
-// 1 - b r is exact in an fma).
-K1_HD double k1_quot(int a, int b) {
-    const double r = (double)k1_rcpf((float)b);
-    const double e = std::fma(-(double)b, r, 1.0);
-    return (double)a * std::fma(r, e, r);
+// The reciprocals a pixel needs, per k in [1, 255] (k1_inv_init; LDS in the
+// kernel): 1 / k rounded to double (h = 60 X / kd and s = kd / kmax as one
+// multiply each, within an ulp of the exact rational) and to float (the
+// half-bin cell's fp32 quotient).  One 16-byte entry, one LDS read.
+struct K1Inv {
+    double inv;
+    float rcp;
+    unsigned pad;
+};
+inline void k1_inv_init(K1Inv* t) {
+    t[0] = K1Inv{0.0, 0.0f, 0u};
+    for (int k = 1; k < 256; k++) t[k] = K1Inv{1.0 / (double)k, 1.0f / (float)k, 0u};
 }
 
 K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
     G.lh = 360 / g.hp;
+    G.rlh = 1.0f / (float)G.lh;
     G.hp = g.hp;
     G.hp2 = 2 * g.hp;
     G.spvp = g.sp * g.vp;
@@ -98,17 +97,29 @@ K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
     }
 }
 
+// c = floor(n2 / (Lh kd1)) for n2 = 120 X < 2^18: (n2 + 1/2) / (Lh kd1) lies
+// at least 1/2 / (Lh kd1) from an integer, and the fp32 form below (1 / Lh
+// times 1 / kd1, each correctly rounded, two products: ~2 ulp) errs by at most
+// (720 / Lh + 1) * 2.4e-7, eight times inside that margin for every Lh <= 360
+// and kd <= 255.
+K1_HD int k1_halfbin(int n2, float rkd, const K1Grid& G) {
+    return (int)(((float)n2 + 0.5f) * G.rlh * rkd);
+}
+
 struct K1Px {
     int cell;        // ncell when deferred
     unsigned lo, hi; // the cell word: lo = 1 | (kmax == 255) << 16, hi = kmax
     double h, s;
 };
 
-// The fast path.  kd = kmx - kmn; code = the table's byte for (kmx, kd).
-// Deferred pixels get cell = ncell (their count and sums land in the dummy
-// cell, never read) and are redone by k1_exact.
+// The fast path.  kd = kmx - kmn; code = the table's byte for (kmx, kd); ekd
+// = the K1Inv entry of max(kd, 1), ikm = 1 / max(kmx, 1) (the caller reads
+// them with the code, ahead of the previous pixels' LDS atomics).  Deferred
+// pixels get cell = ncell (their count and sums land in the dummy cell, never
+// read) and are redone by k1_exact.
 template <bool SMALL>   // SMALL == G.small_c
-K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, const K1Grid& G) {
+K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, const K1Inv& ekd, double ikm,
+                    const K1Grid& G) {
     const int kd1 = kd > 1 ? kd : 1;
     const bool isr = kr == kmx, isg = kg == kmx;
     // X = sector kd + num: rgb2hsv's three branches (max == r first, then g)
@@ -118,7 +129,7 @@ K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, 
     const int X = isr ? xr : xs;
     const int n2 = k1_mul(120, X);
     const int D = k1_mul(G.lh, kd1);
-    const int c = (int)(((float)n2 + 0.5f) * k1_rcpf((float)D));
+    const int c = k1_halfbin(n2, ekd.rcp, G);
     const bool onb = k1_mul(c, D) == n2;
     bool below, def;
     if (SMALL) {
@@ -141,20 +152,21 @@ K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, 
     p.hi = (unsigned)kmx;
     // rgb2hsv: h = 60 X / kd (0 for kd = 0); s = kd / kmx, 0.999999 when
     // min == 0 < max (src/image_processing.c:408-414), 0 for black
-    p.h = k1_quot(k1_mul(60, X), kd1);
-    const double sq = k1_quot(kd, kmx > 1 ? kmx : 1);
-    p.s = (kmn == 0 && kmx != 0) ? 0.999999 : sq;
+    p.h = (double)k1_mul(60, X) * ekd.inv;
+    p.s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * ikm;     // black: kd = 0
     return p;
 }
 
 // A deferred pixel: rgb2hsv's double hue (the reference's expression on the
 // doubles k / 255.0, k255[k]) decides the hue bin ((int)(h / Lh),
 // color_quantization.c:143) and the side of B_c the wrap test puts h on.
+// (k255 == nullptr: k / 255.0 divided here, the same correctly rounded double)
 K1_HD double k1_hue_exact(int kr, int kg, int kb, const double* k255) {
-    const double r = k255[kr], g = k255[kg], b = k255[kb];
+    const double r = k255 ? k255[kr] : (double)kr / 255.0, g = k255 ? k255[kg] : (double)kg / 255.0,
+                 b = k255 ? k255[kb] : (double)kb / 255.0;
     const int kmx = kr > kg ? (kr > kb ? kr : kb) : (kg > kb ? kg : kb);
     const int kmn = kr < kg ? (kr < kb ? kr : kb) : (kg < kb ? kg : kb);
-    const double d = k255[kmx] - k255[kmn];
+    const double d = (k255 ? k255[kmx] : (double)kmx / 255.0) - (k255 ? k255[kmn] : (double)kmn / 255.0);
     const bool isr = kr == kmx, isg = kg == kmx;
     const double num = isr ? g - b : (isg ? b - r : r - g);
     const double sector = isr ? 0.0 : (isg ? 2.0 : 4.0);
@@ -171,8 +183,8 @@ K1_HD K1Px k1_exact(int kr, int kg, int kb, int code, double Lh, const double* k
     const bool isr = kr == kmx, isg = kg == kmx;
     const int t1 = isg ? kb - kr : kr - kg;
     const int X = isr ? kg - kb + (kg < kb ? 6 * kd : 0) : (kd << (isg ? 1 : 2)) + t1;
-    const int n2 = 120 * X, D = G.lh * kd1;
-    const int c = (int)(((float)n2 + 0.5f) * k1_rcpf((float)D));   // as k1_pixel: exact
+    const int n2 = 120 * X;
+    const int c = k1_halfbin(n2, 1.0f / (float)kd1, G);             // as k1_pixel: exact
     const double B = (double)c * (double)G.lh * 0.5;
     const int ch = c - G.hp;
     int below;

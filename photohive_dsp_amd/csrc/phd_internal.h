@@ -317,6 +317,10 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 9, 256, 33, 15, 10, 20)    \
     X(3000, 10, 256, 33, 15, 20, 10)   \
     X(3000, 11, 256, 33, 25, 12, 10)   \
+    X(3000, 12, 256, 1, 15, 20, 10)    \
+    X(3000, 13, 256, 1, 15, 10, 20)    \
+    X(3000, 14, 256, 1, 10, 15, 20)    \
+    X(3000, 15, 256, 5, 10, 15, 20)    \
     X(6000, 0, 512, 5, 15, 20, 20)     \
     X(6000, 1, 512, 5, 10, 20, 30)     \
     X(4000, 0, 256, 5, 10, 20, 20)     \
@@ -340,6 +344,20 @@ bool ct_cols_plan(int h, std::vector<int>* radices);
 // `win` when the block adds its window to the image's bins) instead of all
 // na * nr bins: 1.1-14 KB instead of 23 KB of LDS at 72 x 40 bins, which lets
 // two column blocks share a CU where the full table did not fit beside them.
+// The compile-time FFT passes' half-spectrum intermediate (fft_ct.hip): row
+// pair p's tile row of 4 KP elements (KP = ceil((W/2+1) / 2) column pairs,
+// 16 B each) starts at p * ct_row_stride(W), a multiple of 8 elements, so every
+// tile row -- and every pair of 64-byte tiles the column pass's XCD quads
+// share -- begins on a 128-byte line (an unaligned start made the row pass's
+// partial-line stores fetch their lines: +10 MB per 4000x3000 image).
+constexpr int ct_row_stride(int width) { return (4 * (((width / 2 + 1) + 1) / 2) + 7) & ~7; }
+// elements of one image's intermediate, for either FFT layout (+ scratch past
+// the tiles for the row pass's dummy stores)
+inline size_t inter_elems(int height, int width) {
+    const size_t generic = (size_t)(height + 1) * (width / 2 + 2);
+    const size_t ct = (size_t)((height + 1) / 2) * ct_row_stride(width);
+    return (generic > ct ? generic : ct) + 1024;
+}
 constexpr int kColRunsMax = 256;   // entries (runs + sentinel) of one column's list (LDS)
 struct ColBins {
     const uint32_t* runs = nullptr;  // [wf][rstride] runs of one bin id (ColRuns, phd_host.h): global ids

@@ -492,7 +492,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // intermediates fit 128 MB (half the MALL) run as one row and one column
     // launch per group of images (sizes whose row pairs form whole line groups
     // of the row schedule); small images are otherwise bound by per-launch costs
-    const size_t inter_one = sizeof(double2) * ((size_t)(height + 1) * (wf + 1) + 1024);
+    const size_t inter_one = sizeof(double2) * inter_elems(height, width);
     static const bool ctbatch_off = phd_knob("PHD_CT_NO_BATCH") != nullptr;
     const int q_ct = (int)std::min<size_t>((size_t)n, ((size_t)128 << 20) / inter_one);
     const bool ct_batchable = !ctbatch_off && !overlap_env() && !phd_knob("PHD_FFT_PIPE") && n > 1 && q_ct >= 2 &&
@@ -1308,7 +1308,7 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
     const size_t r_spart = r_sums + al(6 * sizeof(unsigned long long));
     const size_t rb = r_spart + al(sizeof(double) * nchunks);
     const size_t ptrs = al(sizeof(void*) * (size_t)n_images);
-    const size_t inter_one = sizeof(double2) * ((size_t)(height + 1) * (wf + 1) + 1024);
+    const size_t inter_one = sizeof(double2) * inter_elems(height, width);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, (size_t)n_images * rb + ptrs) ||
         !ensure_pinned(c, (size_t)n_images * rb + ptrs) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, inter_one))

@@ -60,7 +60,10 @@ def main():
     pairs = [(r, cols[0]) for r in rows] + [(rows[0], c) for c in cols[1:]]
     code = CHILD % {"root": ROOT, "H": a.H, "W": a.W}
     for r, c in pairs:
-        env = dict(os.environ, PHD_CT_ROWS_VARIANT=str(r), PHD_CT_COLS_VARIANT=str(c), PHD_QUIET="1")
+        # the variants are experiment switches: only the ablate build reads them
+        abl = os.path.join(ROOT, "photohive_dsp_amd", "PhotoHive_DSP_lib", "libreport_data_ablate.so")
+        env = dict(os.environ, PHD_CT_ROWS_VARIANT=str(r), PHD_CT_COLS_VARIANT=str(c), PHD_QUIET="1",
+                   PHD_LIB=os.environ.get("PHD_LIB", abl))
         pr = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
         line = [l for l in pr.stdout.splitlines() if l.startswith("RESULT")]
         print(f"rows v{r} cols v{c}: {line[0] if line else 'FAILED rc=%d %s' % (pr.returncode, pr.stderr[-300:])}",
