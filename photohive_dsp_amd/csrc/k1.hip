@@ -448,13 +448,24 @@ constexpr int kLds3 = 160 * 1024 / 3 - 256;   // three blocks per CU
 
 }  // namespace
 
-// copies (log2) of the one-block form (full code table), -1 when it does not fit
-int k1t_cshift(const GridParams& gp, const ClassTables& t) {
-    if (!t.codes_ok) return -1;
+// copies (log2) of the one-block form, -1 when it does not fit: the full code
+// table, else (fine grids: 36/4/5's 3312 hue cells) the triangular one
+static int cshift_full(const GridParams& gp) {
     const int ncell = HueCells::count(gp);
     for (int cs = 3; cs >= 0; cs--)
         if (l_var(gp.tl, ncell, cs, code_bytes<false>()).end <= kLds1) return cs;
     return -1;
+}
+static int cshift_tri1(const GridParams& gp) {
+    const int ncell = HueCells::count(gp);
+    for (int cs = 3; cs >= 0; cs--)
+        if (l_var(gp.tl, ncell, cs, code_bytes<true>()).end <= kLds1) return cs;
+    return -1;
+}
+
+int k1t_cshift(const GridParams& gp, const ClassTables& t) {
+    if (!t.codes_ok) return -1;
+    return std::max(cshift_full(gp), cshift_tri1(gp));
 }
 
 // copies (log2) of the two-block form (triangular code table), -1 when it does not fit
@@ -510,7 +521,7 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
         return hipGetLastError();
     }
     const bool two = cshift2 >= 0 &&
-                     (cshift < 0 || 19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus));
+                     19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus);
     if (two) {                                            // two 512-thread blocks per CU
         const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
         // with two lanes, one block per CU: the other half of each CU stays free
@@ -521,18 +532,17 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     } else {                                              // one 1024-thread block per CU
         const int grid = (int)std::min<long>(nitems, cus);
         // the triangular code table leaves 31 KiB more for lane copies of the
-        // cells (fine grids: 36/4/5's 3312 hue cells)
-        int cs_tri = -1;
-        for (int cs = 3; cs > cshift && cs_tri < 0; cs--)
-            if (l_var(gp.tl, ncell, cs, code_bytes<true>()).end <= kLds1) cs_tri = cs;
-        if (cs_tri > cshift) {
+        // cells (fine grids: 36/4/5's 3312 hue cells only fit with it)
+        const int cs_full = cshift_full(gp), cs_tri = cshift_tri1(gp);
+        if (cs_tri < 0 && cs_full < 0) return hipErrorInvalidValue;   // k1t_cshift said no
+        if (cs_tri > cs_full) {
             const size_t lds = (size_t)l_var(gp.tl, ncell, cs_tri, code_bytes<true>()).end;
             launch_form<1024, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0, a_stride,
                                     h_stride, cs_tri);
         } else {
-            const size_t lds = (size_t)l_var(gp.tl, ncell, cshift, code_bytes<false>()).end;
+            const size_t lds = (size_t)l_var(gp.tl, ncell, cs_full, code_bytes<false>()).end;
             launch_form<1024, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                     a_stride, h_stride, cshift);
+                                     a_stride, h_stride, cs_full);
         }
     }
     return hipGetLastError();

@@ -47,8 +47,8 @@ struct K1Grid {
     int gs;          // gray_start: first gray / black group
     int ncell;       // HueCells::count; cell ncell is the dummy of deferred pixels
     int small_c;     // every c < 64: the boundary properties are bit masks
-    unsigned long long below_m;   // bit c: an exact boundary hue at B_c counts below it
-    unsigned long long defer_m;   // bit c: B_c is not a multiple of 60 (onb pixels defer)
+    unsigned below_m[2];          // bit c (word c / 32): an exact boundary hue at B_c counts below it
+    unsigned defer_m[2];          // bit c: B_c is not a multiple of 60 (onb pixels defer)
 };
 
 // a * b for 0 <= a, b < 2^24 (and a * b < 2^32): one full-rate v_mul_u32_u24
@@ -87,13 +87,13 @@ K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
     G.ncell = 4 * G.gs + (g.ng + 1) * 2 * g.hp;
     // c < 720 / Lh (X < 6 kd)
     G.small_c = (720 + G.lh - 1) / G.lh <= 64;
-    G.below_m = G.defer_m = 0;
+    G.below_m[0] = G.below_m[1] = G.defer_m[0] = G.defer_m[1] = 0u;
     for (int c = 0; c < 64 && G.small_c; c++) {
         const bool mult60 = (c * G.lh) % 120 == 0;            // B_c = c Lh / 2 is a multiple of 60
         const int ch = c - g.hp;
         const bool below = mult60 && ch >= 0 && ((ch & 1) || ch == 0);
-        if (below) G.below_m |= 1ull << c;
-        if (!mult60) G.defer_m |= 1ull << c;
+        if (below) G.below_m[c >> 5] |= 1u << (c & 31);
+        if (!mult60) G.defer_m[c >> 5] |= 1u << (c & 31);
     }
 }
 
@@ -133,8 +133,10 @@ K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, 
     const bool onb = k1_mul(c, D) == n2;
     bool below, def;
     if (SMALL) {
-        below = onb && ((G.below_m >> c) & 1);
-        def = onb && ((G.defer_m >> c) & 1);
+        // 32-bit words (a 64-bit shift and compare cost several VALU slots)
+        const bool hi = c >= 32;
+        below = onb && (((hi ? G.below_m[1] : G.below_m[0]) >> (c & 31)) & 1u);
+        def = onb && (((hi ? G.defer_m[1] : G.defer_m[0]) >> (c & 31)) & 1u);
     } else {
         const bool special = (kr == kg) | (kg == kb) | (kr == kb);
         const int ch = c - G.hp;

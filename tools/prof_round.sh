@@ -1,13 +1,24 @@
-# One profiling round on the GPU box (run through gpurun from the repo root):
-# PMC HBM traffic per kernel (separate FETCH_SIZE / WRITE_SIZE passes), the
+# One measurement round on the GPU box (run through gpurun from the repo root):
+# the GPU test suite, K1's batch timing, the FETCH_SIZE calibrations and the
+# per-kernel PMC traffic (separate FETCH_SIZE / WRITE_SIZE passes), the
 # rocprofv3 kernel statistics of config 2 alone and of the default bench
-# command, and the full bench line.  Copy the results into profiles/rNN/.
-set -e
-TAG="${1:-r03}"
+# command, and the default bench line.  Stops at the first crash / timeout
+# (tools/gpu_run.sh).  Copy the results into profiles/rNN/.
+#   bash tools/prof_round.sh r04 [steps...]   (steps: tests k1 calib pmc prof bench; default all)
+TAG="${1:-r04}"; shift
+STEPS="${*:-tests k1 calib pmc prof bench}"
 mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python tools/pmc_collect.py --tag "${TAG:-r03}" -- --steps 3 --warmup 1 --no-config3 --batch 8 > gpurun_out/pmc_collect.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof2 -o prof -- python bench.py --no-config3 --no-cpu-baseline > gpurun_out/bench_prof2.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline > gpurun_out/bench_prof.log 2>&1
-timeout -k 10 300 python bench.py > gpurun_out/bench_full.log 2>&1
-tail -1 gpurun_out/bench_full.log
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+args=()
+for s in $STEPS; do
+  case $s in
+    tests) args+=("gputest:900:python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider");;
+    k1) args+=("k1bench:200:python -u tools/k1bench.py");;
+    calib) args+=("pmc_calib:400:python tools/pmc_calib.py");;
+    pmc) args+=("pmc_collect:400:python tools/pmc_collect.py --tag $TAG -- --steps 3 --warmup 1 --no-configs --batch 8");;
+    prof) args+=("prof_config2:400:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof2 -o prof -- python bench.py --no-configs --no-cpu-baseline"
+                 "prof_default:500:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline");;
+    bench) args+=("bench_full:500:python bench.py");;
+  esac
+done
+bash tools/gpu_run.sh "${args[@]}"
