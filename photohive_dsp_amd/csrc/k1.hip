@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "k1_pixel.h"
@@ -100,14 +101,24 @@ struct Mom {
     unsigned sr, sg, sb, qr, qg, qb;
 };
 
+// A thread's run of pixels in one hue cell (MERGE): consecutive pixels of a
+// thread that land in the same cell are summed in registers and added to the
+// LDS with one set of atomics when the cell changes (flat image regions put
+// most of a wave's lanes on one address, where LDS atomics serialise).
+struct CellRun {
+    int cell;            // -1: empty
+    unsigned lo, hi;
+    double h, s;
+};
+
 // 4 pixels (one dwordx3): moments, then each pixel classified and counted;
 // bit i of the result = pixel i deferred.
-template <bool TRI, bool SMALL>
+template <bool TRI, bool SMALL, bool RT, bool MERGE = false>
 __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
                                              const unsigned char* __restrict__ code8,
                                              const K1Inv* __restrict__ inv,
                                              unsigned char* __restrict__ cells, int cshift, int copy,
-                                             const K1Grid& G) {
+                                             const K1Grid& G, CellRun* run = nullptr, unsigned* same = nullptr) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
     const u16x2 r13 = as2(__builtin_amdgcn_perm(w2, w0, 0x0c050c03u));
@@ -148,8 +159,10 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
-        ekd[i] = inv[kd > 1 ? kd : 1];
-        ikm[i] = inv[kmx > 1 ? kmx : 1].inv;
+        // RT: the LDS table (two more LDS reads per pixel); else the VALU
+        // (measured faster: 40 against 46 us per image, the LDS is the busier)
+        ekd[i] = RT ? inv[kd > 1 ? kd : 1] : k1_inv_valu(kd > 1 ? kd : 1);
+        ikm[i] = RT ? inv[kmx > 1 ? kmx : 1].inv : k1_inv_valu(kmx > 1 ? kmx : 1).inv;
     }
     unsigned def = 0;
 #pragma unroll
@@ -158,13 +171,39 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
         const int kr = (R[q] >> sh) & 0xFFFF, kg = (Gc[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
         const K1Px p = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kd, code[i], ekd[i], ikm[i], G);
-        cell_add(cells, p.cell, cshift, copy, p);
+        if constexpr (MERGE) {
+            if (p.cell == run->cell) {
+                run->lo += p.lo;
+                run->hi += p.hi;
+                run->h += p.h;
+                run->s += p.s;
+            } else {
+                if (run->cell >= 0) {
+                    K1Px q;
+                    q.lo = run->lo; q.hi = run->hi; q.h = run->h; q.s = run->s;
+                    cell_add(cells, run->cell, cshift, copy, q);
+                }
+                *run = CellRun{p.cell, p.lo, p.hi, p.h, p.s};
+            }
+        } else {
+            cell_add(cells, p.cell, cshift, copy, p);
+        }
         def |= (unsigned)(p.cell == G.ncell) << i;
+        if (same) {                                       // all four pixels in one cell (the MG 2 sample)
+            if (i == 0) *same = (unsigned)p.cell;
+            else if (*same != (unsigned)p.cell) *same = ~0u;
+        }
     }
+    if (same) *same = *same != ~0u;
     return def;
 }
 
-template <int KT, bool TRI, bool SMALL, int MINW = 4, bool LEAN = false>
+// MG: 0 every pixel's atomics; 1 per-thread cell runs (CellRun); 2 cell runs
+// for the next chunk when more than a fifth of this chunk's sampled 4-pixel
+// groups (each thread's first) lie in one cell, else per pixel -- flat images
+// (SURVEY 8(d) row 2(b)'s blurred structured ones: 81 % of groups) pay for
+// the runs' selects, noise does not.
+template <int KT, bool TRI, bool SMALL, int MINW = 4, bool LEAN = false, bool RT = false, int MG = 0>
 __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restrict__ imgs, long npix, int nchunks,
                                                long nitems, GridParams gp, K1Grid G,
                                                const ClassTables* __restrict__ tabs,
@@ -185,6 +224,9 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
     // the three-block form (MINW 6) has no LDS k / 255 table: k1_exact divides
     double* k255 = MINW > 4 ? nullptr : reinterpret_cast<double*>(smem + V.k255);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + V.red);
+    // MG 2: the two chunk-parity vote counters, past the 8 waves' flush records
+    unsigned* vote = reinterpret_cast<unsigned*>(red + 120);
+    int merge = 0, vpar = 0;                                    // block-uniform
     unsigned* rcell = reinterpret_cast<unsigned*>(smem + V.rcell);
     unsigned* cg = reinterpret_cast<unsigned*>(smem + V.cg);
     unsigned* seg = reinterpret_cast<unsigned*>(smem + V.seg);
@@ -203,6 +245,7 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
         unsigned* z = reinterpret_cast<unsigned*>(smem);
         for (int i = tid; i < V.code / 4; i += kT) z[i] = 0u;                        // cells
         for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;           // run records
+        if (tid < 2) vote[tid] = 0u;
     }
     // the (0, 0, 0) pixel's cell: masked groups past the image end are zero
     // pixels (c = 0, not below)
@@ -278,19 +321,37 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
             };
             unsigned a0, a1, a2;
             ld(0, a0, a1, a2);
+            CellRun run{-1, 0u, 0u, 0.0, 0.0};
+            unsigned same0 = 0;
+            auto loop = [&](auto mg) __attribute__((always_inline)) {
+                constexpr bool M = decltype(mg)::value;
 #pragma unroll 1
-            for (int st = 0; st < kG; st++) {
-                unsigned n0 = 0, n1 = 0, n2 = 0;
-                if (st + 1 < kG) ld(st + 1, n0, n1, n2);
-                emask |= k1_group<TRI, SMALL>(a0, a1, a2, m, code8, inv, cells, cshift, copy, G) << (4 * st);
-                a0 = n0;
-                a1 = n1;
-                a2 = n2;
+                for (int st = 0; st < kG; st++) {
+                    unsigned n0 = 0, n1 = 0, n2 = 0;
+                    if (st + 1 < kG) ld(st + 1, n0, n1, n2);
+                    emask |= k1_group<TRI, SMALL, RT, M>(a0, a1, a2, m, code8, inv, cells, cshift, copy, G, &run,
+                                                         (MG == 2 && st == 0) ? &same0 : nullptr)
+                             << (4 * st);
+                    a0 = n0;
+                    a1 = n1;
+                    a2 = n2;
+                }
+                if (M && run.cell >= 0) {
+                    K1Px q;
+                    q.lo = run.lo; q.hi = run.hi; q.h = run.h; q.s = run.s;
+                    cell_add(cells, run.cell, cshift, copy, q);
+                }
+            };
+            if (MG == 1 || (MG == 2 && merge)) loop(std::true_type{});
+            else loop(std::false_type{});
+            if constexpr (MG == 2) {
+                const unsigned long long b = __ballot(same0);
+                if (lane_id() == 0) atomicAdd(&vote[vpar], (unsigned)__popcll(b));
             }
         } else {
 #pragma unroll
             for (int st = 0; st < kG; st++)
-                emask |= k1_group<TRI, SMALL>(cw[st][0], cw[st][1], cw[st][2], m, code8, inv, cells, cshift, copy, G)
+                emask |= k1_group<TRI, SMALL, RT>(cw[st][0], cw[st][1], cw[st][2], m, code8, inv, cells, cshift, copy, G)
                          << (4 * st);
         }
         const bool last_chunk = base + kChunk >= npix;            // block-uniform
@@ -327,6 +388,7 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
             atomicAdd(reinterpret_cast<unsigned long long*>(cells + kCellBytes * (zcell << cshift)),
                       (unsigned long long)(-pad));
         __syncthreads();
+        if constexpr (MG == 2) merge = 5 * vote[vpar] > (unsigned)kT;   // the next chunk's mode
         // fold the chunk's count words: one thread per cell sums its C copies;
         // the run's cell counts, the chunk's group counts, per-group sum kmax / n255
         for (int q = tid; q <= ncell; q += kT) {
@@ -346,6 +408,10 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
             }
         }
         __syncthreads();
+        if constexpr (MG == 2) {
+            if (tid == 0) vote[vpar] = 0u;                        // read by every thread before this barrier
+            vpar ^= 1;
+        }
         unsigned short* chunk_out =
             reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(out.chunk_hist) + cimg * h_stride) +
             (long)cc * tl;
@@ -430,15 +496,15 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
     }
 }
 
-template <int KT, bool TRI, int MINW = 4, bool LEAN = false>
+template <int KT, bool TRI, int MINW = 4, bool LEAN = false, bool RT = false, int MG = 0>
 void launch_form(int grid, size_t lds, hipStream_t st, const uint8_t* const* d_imgs, long npix, int nchunks,
                  long nitems, const GridParams& gp, const K1Grid& G, const ClassTables* tabs, const double* k255,
                  const PaletteDev& out0, long a_stride, long h_stride, int cshift) {
     if (G.small_c)
-        phd_launch((k_k1t<KT, TRI, true, MINW, LEAN>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
+        phd_launch((k_k1t<KT, TRI, true, MINW, LEAN, RT, MG>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
                    gp, G, tabs, k255, out0, a_stride, h_stride, cshift);
     else
-        phd_launch((k_k1t<KT, TRI, false, MINW, LEAN>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
+        phd_launch((k_k1t<KT, TRI, false, MINW, LEAN, RT, MG>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
                    gp, G, tabs, k255, out0, a_stride, h_stride, cshift);
 }
 
@@ -491,7 +557,13 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                             (const void*)k_k1t<1024, true, true>,  (const void*)k_k1t<1024, true, false>,
                             (const void*)k_k1t<512, true, true>,   (const void*)k_k1t<512, true, false>,
                             (const void*)k_k1t<512, true, true, 6, true>, (const void*)k_k1t<512, true, false, 6, true>,
-                            (const void*)k_k1t<512, true, true, 4, true>, (const void*)k_k1t<512, true, false, 4, true>};
+                            (const void*)k_k1t<512, true, true, 4, true>, (const void*)k_k1t<512, true, false, 4, true>,
+                            (const void*)k_k1t<512, true, true, 4, true, true>,
+                            (const void*)k_k1t<512, true, false, 4, true, true>,
+                            (const void*)k_k1t<512, true, true, 4, true, false, 1>,
+                            (const void*)k_k1t<512, true, false, 4, true, false, 1>,
+                            (const void*)k_k1t<512, true, true, 4, true, false, 2>,
+                            (const void*)k_k1t<512, true, false, 4, true, false, 2>};
         for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -513,6 +585,20 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                                         a_stride, h_stride, 0);
         return hipGetLastError();
     }
+    if (form == 7 && cshift2 >= 0) {                         // the two-block form with per-thread cell runs
+        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
+        const int grid = (int)std::min<long>(nitems, 2 * cus);
+        launch_form<512, true, 4, true, false, 1>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
+                                                  k255, out0, a_stride, h_stride, cshift2);
+        return hipGetLastError();
+    }
+    if (form == 6 && cshift2 >= 0) {                         // the two-block form with the LDS reciprocal table
+        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
+        const int grid = (int)std::min<long>(nitems, 2 * cus);
+        launch_form<512, true, 4, true, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
+                                              a_stride, h_stride, cshift2);
+        return hipGetLastError();
+    }
     if (form == 5 && cshift2 >= 0) {
         const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
         const int grid = (int)std::min<long>(nitems, 2 * cus);
@@ -520,15 +606,19 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                                          a_stride, h_stride, cshift2);
         return hipGetLastError();
     }
-    const bool two = cshift2 >= 0 &&
+    const bool two = cshift2 >= 0 && form != 1 &&            // PHD_K1_FORM=1: the one-block form (experiment)
                      19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus);
     if (two) {                                            // two 512-thread blocks per CU
         const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
         // with two lanes, one block per CU: the other half of each CU stays free
         // for the other lane's FFT blocks (k1_blocks_per_cu)
         const int grid = (int)std::min<long>(nitems, (long)k1_blocks_per_cu() * cus);
-        launch_form<512, true, 4, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                        a_stride, h_stride, cshift2);
+        if (form == 8)                                    // per-pixel atomics always (experiment)
+            launch_form<512, true, 4, true, false, 0>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
+                                                      k255, out0, a_stride, h_stride, cshift2);
+        else
+            launch_form<512, true, 4, true, false, 2>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
+                                                      k255, out0, a_stride, h_stride, cshift2);
     } else {                                              // one 1024-thread block per CU
         const int grid = (int)std::min<long>(nitems, cus);
         // the triangular code table leaves 31 KiB more for lane copies of the
@@ -558,14 +648,12 @@ int k1_host_pixels(const GridParams& gp, const ClassTables& t, const uint8_t* rg
     k1_grid_init(G, gp);
     double k255[256];
     for (int k = 0; k < 256; k++) k255[k] = (double)k / 255.0;
-    K1Inv inv[256];
-    k1_inv_init(inv);
     for (long i = 0; i < n; i++) {
         const int kr = rgb[3 * i], kg = rgb[3 * i + 1], kb = rgb[3 * i + 2];
         const int kmx = std::max(kr, std::max(kg, kb)), kmn = std::min(kr, std::min(kg, kb)), kd = kmx - kmn;
         const int code = t.code8[kmx * 256 + kd];
-        const K1Inv& ekd = inv[kd > 1 ? kd : 1];
-        const double ikm = inv[kmx > 1 ? kmx : 1].inv;
+        const K1Inv ekd = k1_inv_valu(kd > 1 ? kd : 1);          // as the production kernel (RT false)
+        const double ikm = k1_inv_valu(kmx > 1 ? kmx : 1).inv;
         K1Px p = G.small_c ? k1_pixel<true>(kr, kg, kb, kmx, kmn, kd, code, ekd, ikm, G)
                            : k1_pixel<false>(kr, kg, kb, kmx, kmn, kd, code, ekd, ikm, G);
         const bool def = p.cell == G.ncell;

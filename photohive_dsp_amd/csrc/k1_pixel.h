@@ -70,6 +70,18 @@ struct K1Inv {
     float rcp;
     unsigned pad;
 };
+// The same entry from the VALU: the fp32 reciprocal and one fp64 Newton step
+// (1 - k r is exact in an fma; ~2^-45 relative), no table read.
+K1_HD K1Inv k1_inv_valu(int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float r = __builtin_amdgcn_rcpf((float)k);
+#else
+    const float r = 1.0f / (float)k;
+#endif
+    const double d = (double)r;
+    const double e = std::fma(-(double)k, d, 1.0);
+    return K1Inv{std::fma(d, e, d), r, 0u};
+}
 inline void k1_inv_init(K1Inv* t) {
     t[0] = K1Inv{0.0, 0.0f, 0u};
     for (int k = 1; k < 256; k++) t[k] = K1Inv{1.0 / (double)k, 1.0f / (float)k, 0u};

@@ -10,10 +10,16 @@ from photohive_dsp_amd.core import make_config
 from photohive_dsp_amd.structures import Full_Report_Data, RGB_Statistics
 
 
+KIND = os.environ.get("K1KIND", "uniform")          # or hblur: SURVEY 8(d) row 2(b)'s structured images
+
+
 def fill(n, h, w):
     t = torch.empty(n * h * w * 3, dtype=torch.uint8, device="cuda")
     for i in range(n):
-        assert lib.phd_fill_uniform_device(t[i * h * w * 3:].data_ptr(), h * w * 3, i, None) == 0
+        if KIND == "hblur":
+            assert lib.phd_fill_structured_device(t[i * h * w * 3:].data_ptr(), h, w, 2 + i, 15, 1, None) == 0
+        else:
+            assert lib.phd_fill_uniform_device(t[i * h * w * 3:].data_ptr(), h * w * 3, i, None) == 0
     return t
 
 
@@ -23,7 +29,7 @@ def k1_avg():
     return 1000 * tot.value / max(cnt.value, 1)
 
 
-tag = os.environ.get("PHD_LIB", "default")
+tag = os.environ.get("PHD_LIB", "default").split("/")[-1] + f" {KIND}" + (f" form {os.environ['PHD_K1_FORM']}" if os.environ.get("PHD_K1_FORM") else "")
 for n, h, w in [(64, 1080, 1920), (512, 1080, 1920)]:
     t = fill(n, h, w)
     st = (RGB_Statistics * n)()
