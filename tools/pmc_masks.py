@@ -18,7 +18,7 @@ NAME = {1: "k_rows_ct", 2: "k_cols_ct"}
 
 def run(counter, kernel, masks):
     out = os.path.join(ROOT, "gpurun_out", f"pmc_masks_{kernel}_{counter}")
-    env = dict(os.environ, PHD_LIB=ABL)
+    env = dict(os.environ, PHD_LIB=os.environ.get("PMC_LIB", ABL))
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "p", "--",
            sys.executable, os.path.join(ROOT, "tools", "kbench.py"), str(kernel)] + [str(m) for m in masks]
     subprocess.run(cmd, cwd=ROOT, env=env, check=True, timeout=170)

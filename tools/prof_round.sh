@@ -22,3 +22,9 @@ for s in $STEPS; do
   esac
 done
 bash tools/gpu_run.sh "${args[@]}"
+rc=$?
+# only the summaries travel back (gpurun copies at most 64 MiB of gpurun_out/)
+find gpurun_out -name "*kernel_trace.csv" -delete 2>/dev/null
+find gpurun_out -path "*pmc_*" -name "*counter_collection.csv" -size +4M -delete 2>/dev/null
+du -sh gpurun_out
+exit $rc
