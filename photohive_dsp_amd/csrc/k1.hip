@@ -224,8 +224,9 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
     // the three-block form (MINW 6) has no LDS k / 255 table: k1_exact divides
     double* k255 = MINW > 4 ? nullptr : reinterpret_cast<double*>(smem + V.k255);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + V.red);
-    // MG 2: the two chunk-parity vote counters, past the 8 waves' flush records
-    unsigned* vote = reinterpret_cast<unsigned*>(red + 120);
+    // MG 2: the two chunk-parity vote counters, in the unused slot 7 of waves 0
+    // and 1's flush records (vote[0], vote[16])
+    unsigned* vote = reinterpret_cast<unsigned*>(red + 7);
     int merge = 0, vpar = 0;                                    // block-uniform
     unsigned* rcell = reinterpret_cast<unsigned*>(smem + V.rcell);
     unsigned* cg = reinterpret_cast<unsigned*>(smem + V.cg);
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
         unsigned* z = reinterpret_cast<unsigned*>(smem);
         for (int i = tid; i < V.code / 4; i += kT) z[i] = 0u;                        // cells
         for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;           // run records
-        if (tid < 2) vote[tid] = 0u;
+        if (tid < 2) vote[16 * tid] = 0u;
     }
     // the (0, 0, 0) pixel's cell: masked groups past the image end are zero
     // pixels (c = 0, not below)
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
             else loop(std::false_type{});
             if constexpr (MG == 2) {
                 const unsigned long long b = __ballot(same0);
-                if (lane_id() == 0) atomicAdd(&vote[vpar], (unsigned)__popcll(b));
+                if (lane_id() == 0) atomicAdd(&vote[16 * vpar], (unsigned)__popcll(b));
             }
         } else {
 #pragma unroll
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
             atomicAdd(reinterpret_cast<unsigned long long*>(cells + kCellBytes * (zcell << cshift)),
                       (unsigned long long)(-pad));
         __syncthreads();
-        if constexpr (MG == 2) merge = 5 * vote[vpar] > (unsigned)kT;   // the next chunk's mode
+        if constexpr (MG == 2) merge = 5 * vote[16 * vpar] > (unsigned)kT;   // the next chunk's mode
         // fold the chunk's count words: one thread per cell sums its C copies;
         // the run's cell counts, the chunk's group counts, per-group sum kmax / n255
         for (int q = tid; q <= ncell; q += kT) {
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
         }
         __syncthreads();
         if constexpr (MG == 2) {
-            if (tid == 0) vote[vpar] = 0u;                        // read by every thread before this barrier
+            if (tid == 0) vote[16 * vpar] = 0u;                        // read by every thread before this barrier
             vpar ^= 1;
         }
         unsigned short* chunk_out =
@@ -563,7 +564,11 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                             (const void*)k_k1t<512, true, true, 4, true, false, 1>,
                             (const void*)k_k1t<512, true, false, 4, true, false, 1>,
                             (const void*)k_k1t<512, true, true, 4, true, false, 2>,
-                            (const void*)k_k1t<512, true, false, 4, true, false, 2>};
+                            (const void*)k_k1t<512, true, false, 4, true, false, 2>,
+                            (const void*)k_k1t<1024, true, true, 4, true, false, 2>,
+                            (const void*)k_k1t<1024, true, false, 4, true, false, 2>,
+                            (const void*)k_k1t<1024, false, true, 4, true, false, 2>,
+                            (const void*)k_k1t<1024, false, false, 4, true, false, 2>};
         for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -625,14 +630,23 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
         // cells (fine grids: 36/4/5's 3312 hue cells only fit with it)
         const int cs_full = cshift_full(gp), cs_tri = cshift_tri1(gp);
         if (cs_tri < 0 && cs_full < 0) return hipErrorInvalidValue;   // k1t_cshift said no
+        // (form 9, experiment: the round-3 loop with the whole next chunk in registers)
         if (cs_tri > cs_full) {
             const size_t lds = (size_t)l_var(gp.tl, ncell, cs_tri, code_bytes<true>()).end;
-            launch_form<1024, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0, a_stride,
-                                    h_stride, cs_tri);
+            if (form == 9)
+                launch_form<1024, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
+                                        a_stride, h_stride, cs_tri);
+            else
+                launch_form<1024, true, 4, true, false, 2>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
+                                                           k255, out0, a_stride, h_stride, cs_tri);
         } else {
             const size_t lds = (size_t)l_var(gp.tl, ncell, cs_full, code_bytes<false>()).end;
-            launch_form<1024, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                     a_stride, h_stride, cs_full);
+            if (form == 9)
+                launch_form<1024, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
+                                         a_stride, h_stride, cs_full);
+            else
+                launch_form<1024, false, 4, true, false, 2>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G,
+                                                            tabs, k255, out0, a_stride, h_stride, cs_full);
         }
     }
     return hipGetLastError();
