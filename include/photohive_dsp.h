@@ -238,10 +238,6 @@ int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int height, int widt
 int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int width, double* d_out);
 /* log_mant, the polar bins' table-driven fp64 log, over n positive device doubles. */
 int phd_debug_log_mant(const double* d_x, double* d_y, long n);
-/* The compile-time column pass's per-block bin windows: 0 off, 1 where they
- * raise occupancy (default), 2 always; -1 only queries.  Returns the previous
- * mode; takes effect at the next call's FFT selection. */
-int phd_debug_col_windows(int mode);
 
 /* Validation hook for the global-memory FFTs behind sides above 8192 px and
  * lengths with a large prime factor (the reference's FFTW r2c takes any

@@ -77,18 +77,19 @@ __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
 // run whose sum of log p is the log of its product: the frexp mantissas
 // multiply (>= 2^-E, no underflow), the exponents add, and one fp64 log
 // closes the run (pgm_normalize_fft's fp64 log, src/fft_processing.c:
-// 196-199).  Each run adds bin_scale fixed point to its bin with one LDS
-// atomic (order-independent sums).  A thread's first two runs are kept in
+// 196-199).  Each run adds bin_scale fixed point to its run's LDS slot (sl,
+// indexed like rl) with one LDS atomic (order-independent sums); the block
+// adds the column's slots to the image's bins afterwards.  A thread's first two runs are kept in
 // registers and logged after the walk: a wave then evaluates the fp64 log at
 // most twice (plus the rare third run of a thread), where logging inside the
 // unrolled walk ran it on almost every row (some lane of 64 changes bin there).
 template <int E>
 __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0, int rend, const unsigned* rl,
-                                          int idx, unsigned long long* bsum, double bscale,
+                                          int idx, unsigned long long* sl, double bscale,
                                           const double2* __restrict__ lt) {
-    auto flush = [&](int b, double m, int e) {
+    auto flush = [&](int k, double m, int e) {
         const double acc = fmax((double)e * 0.69314718055994530942 + log_mant(m, lt), 0.0);
-        atomicAdd(&bsum[b], bin_fixed(acc, bscale));
+        atomicAdd(&sl[k], bin_fixed(acc, bscale));
     };
     if (r0 >= rend) return;
     // the thread's first four entries in registers (one LDS latency), refilled
@@ -97,7 +98,8 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
     const unsigned q0 = rl[idx];
     unsigned q1 = rl[idx + 1], q2 = rl[min(idx + 2, kColRunsMax - 1)], q3 = rl[min(idx + 3, kColRunsMax - 1)];
     int qi = idx + 4;
-    int cur = (int)(q0 & 0xFFFFu), nxt = (int)(q1 >> 16);
+    int cur = idx, nxt = (int)(q1 >> 16);                   // cur: the run's slot
+    (void)q0;
     int esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
     double mprod = 1.0, m0 = 1.0, m1 = 1.0;
     auto close = [&]() {
@@ -116,7 +118,7 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
             const double pv = lgb[r];
             if (r >= nxt) {                       // the next run starts here (runs are never empty)
                 close();
-                cur = (int)(q1 & 0xFFFFu);
+                cur++;
                 q1 = q2;
                 q2 = q3;
                 q3 = rl[min(qi++, kColRunsMax - 1)];
@@ -132,21 +134,6 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
     close();
     if (n > 0) flush(b0, m0, e0);
     if (n > 1) flush(b1, m1, e1);
-}
-
-// The block's LDS bins into the image's sums (one atomic per non-zero bin).
-// With windows (win != nullptr) an LDS id is local to the block's rectangle of
-// (angle, radius) bins: global = first + (i / width) * nr + i % width.
-__device__ __forceinline__ void flush_bins(const unsigned long long* lb, int nlb, const int* __restrict__ win, int nr,
-                                           unsigned long long* __restrict__ bin_sums, int tid, int nt) {
-    const int first = win ? win[2 * blockIdx.x] : 0, width = win ? win[2 * blockIdx.x + 1] : 1;
-    for (int i = tid; i < nlb; i += nt) {
-        const unsigned long long t = lb[i];
-        if (t != 0ull) {
-            const int a = win ? i / width : 0;
-            atomicAdd(&bin_sums[win ? first + a * nr + (i - a * width) : i], t);
-        }
-    }
 }
 
 template <int W, int T, int... Rs>
@@ -339,15 +326,20 @@ struct ColK {
     // the run lists of the block's columns (ColRuns): kColRunsMax entries each,
     // RPT per thread
     static constexpr int RPT = (kColRunsMax + T - 1) / T;
-    static size_t lds(int nbins) {
-        return sizeof(double2) * (NC * H + NTW + kLogTab) + sizeof(unsigned) * NC * kColRunsMax +
-               (GB ? 0 : sizeof(unsigned long long) * nbins);
+    // + per column its run list and one u64 slot per run (the bins are summed
+    // per run, then added to the image's bins column by column: no LDS array
+    // of all na x nr bins)
+    static size_t lds(int) {
+        return sizeof(double2) * (NC * H + NTW + kLogTab) + (sizeof(unsigned) + sizeof(unsigned long long)) * NC *
+                                                                kColRunsMax;
     }
     static_assert(Radices<Rs...>::product == H, "plan");
     // waves per SIMD of the launch bounds: one-column blocks are sized for two
     // resident blocks per CU, one when the column and twiddles fill the LDS
     static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
-    static constexpr int MINW = (CPB & 16) ? (3 * ((T + 63) / 64) + 3) / 4 : (NC == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2 : 1);
+    // 64: sized for three resident one-column blocks per CU (168 VGPRs; the
+    // LDS holds three 3000-row columns now that the bins are per run)
+    static constexpr int MINW = (CPB & 64) ? 3 : (CPB & 16) ? (3 * ((T + 63) / 64) + 3) / 4 : (NC == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2 : 1);
     static_assert(NC == 1 || NC == 2, "columns per block");
     static_assert(!P0R || (NC == 1 && PF && PE::NB <= T && Radices<Rs...>::count >= 2), "pass 0 from registers");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
@@ -362,7 +354,6 @@ template <int H, int T, int CPB, int... Rs>
 __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
                                                      const unsigned* __restrict__ runs,
                                                      const uint8_t* __restrict__ segidx, int rstride, int nbins,
-                                                     const int* __restrict__ win, int nr,
                                                      unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums0, int width,
@@ -377,8 +368,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     double2* bufs = reinterpret_cast<double2*>(smem);         // [CPB][H]
     double2* tw = bufs + NC * H;
     double2* lt = tw + K::NTW;                                 // log_mant's table
-    unsigned* rbuf = reinterpret_cast<unsigned*>(lt + kLogTab);          // [NC][kColRunsMax]
-    unsigned long long* lb = reinterpret_cast<unsigned long long*>(rbuf + NC * kColRunsMax);
+    unsigned long long* slots = reinterpret_cast<unsigned long long*>(lt + kLogTab);   // [NC][kColRunsMax]
+    unsigned* rbuf = reinterpret_cast<unsigned*>(slots + NC * kColRunsMax);         // [NC][kColRunsMax]
     const int tid = threadIdx.x;
     // a batch: nimg images of one size, their intermediates, bin sums, max
     // partials and channel sums istride / bstride / fstride / sstride apart;
@@ -395,10 +386,8 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     const int ht = NC == 2 ? tid - half * T : tid;
     double2* buf = bufs + (NC == 2 ? half * H : 0);
     for (int i = tid; i < K::NTW; i += NT) tw[i] = twg[i];
-    if (!K::GB)
-        for (int i = tid; i < nbins; i += NT) lb[i] = 0ull;
+    for (int i = tid; i < NC * kColRunsMax; i += NT) slots[i] = 0ull;
     log_table_init(lt, tid, NT);
-    unsigned long long* bsum = K::GB ? bin_sums : lb;         // where the runs are added
     const int kpn = (wf + 1) / 2;
     const size_t rs = (size_t)((4 * kpn + 7) & ~7);           // row-pair stride (ct_row_stride)
     const int nunit = (kpn + 1) / 2;                          // tile pairs (128-byte lines)
@@ -453,7 +442,6 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     bin_sums = bin_sums0 + im * bstride;
     fmax_part = fmax_part0 + im * fstride;
     sums = sums0 + im * sstride;
-    if (K::GB) bsum = bin_sums;
     if (K::P0R && u0 < un) fetch0(pair_at(u0));
     else if (K::PF && u0 < un) PHD_COL_FETCH(pair_at(u0));
     double mx = 0.0;
@@ -550,8 +538,25 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
-        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, rl, sidx, bsum, bscale, lt);
+        unsigned long long* sl = slots + (NC == 2 ? half * kColRunsMax : 0);
+        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, rl, sidx, sl, bscale, lt);
         __syncthreads();
+        // the column's run sums into the image's bins (a bin met by two runs of
+        // a column gets two atomics); entries past the sentinel start at H
+        if (!(ablate & 8)) {
+#pragma unroll
+            for (int k = 0; k < K::RPT; k++) {
+                const int t = ht + k * T;
+                if (t < kColRunsMax && t < rstride) {
+                    const unsigned e = rl[t];
+                    const unsigned long long v = sl[t];
+                    if ((int)(e >> 16) < H && v) {
+                        sl[t] = 0ull;
+                        atomicAdd(&bin_sums[e & 0xFFFFu], v);
+                    }
+                }
+            }
+        }
     }
 #undef PHD_COL_FETCH
     // block max -> one partial per block; non-zero bins -> the image's sums
@@ -564,14 +569,7 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
         for (int w = 0; w < (NT + 63) / 64; w++) m = fmax(m, red[w]);
         fmax_part[blockIdx.x] = m;
     }
-    if (!K::GB && !(ablate & 8)) flush_bins(lb, nbins, win, nr, bin_sums, tid, NT);
-    if (seg < c1) {
-        // the next image's bins start from zero (each thread clears the entries
-        // it flushed); red (in the buffer) is free after this barrier
-        if (!K::GB)
-            for (int i = tid; i < nbins; i += NT) lb[i] = 0ull;
-        __syncthreads();
-    }
+    if (seg < c1) __syncthreads();                             // red (in the buffer) is reused
     }
 }
 
@@ -629,40 +627,13 @@ hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, u
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st, int nimg = 1, long istride = 0, long bstride = 0, long fstride = 0,
                    long sstride = 0) {
-    const size_t lds = cols_lds<H, T, CPB, Rs...>(cb.nlb);
-    const int grid = cb.grid > 0 ? cb.grid : cols_grid<H, T, CPB, Rs...>(wf, cb.nlb);
+    const size_t lds = cols_lds<H, T, CPB, Rs...>(0);
+    const int grid = cols_grid<H, T, CPB, Rs...>(wf, 0);
     phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.runs, cb.seg,
-               cb.rstride, cb.nlb,
-               cb.win, cb.nr, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg, istride,
+               cb.rstride, 0,
+               bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg, istride,
                bstride, fstride, sstride);
     return hipGetLastError();
-}
-
-// Which block processes each column (the kernels' schedules above): one
-// column per block, blocks b, b^8, b^16, b^24 taking the four columns of a
-// line; or a tile (two columns) per block, blocks b, b^8 the two tiles.
-template <int H, int T, int CPB, int... Rs>
-void cols_owners(int wf, int grid, std::vector<int>* owner) {
-    owner->assign(wf, -1);
-    const int kpn = (wf + 1) / 2, nunit = (kpn + 1) / 2;
-    const bool pairs = (CPB & 3) == 2;
-    for (int b = 0; b < grid; b++) {
-        const int q = pairs ? (b >> 3) & 1 : (b >> 3) & 3;
-        const int nlog = pairs ? grid / 2 : grid / 4;
-        const int lblk = pairs ? (b >> 4) * 8 + (b & 7) : (b >> 5) * 8 + (b & 7);
-        const int c0 = (int)((long)lblk * nunit / nlog), c1 = (int)((long)(lblk + 1) * nunit / nlog);
-        for (int u = c0; u < c1; u++) {
-            if (pairs) {
-                for (int g = 0; g < 2; g++) {
-                    const int col = 2 * (2 * u + q) + g;
-                    if (col < wf) (*owner)[col] = b;
-                }
-            } else {
-                const int col = 2 * (2 * u + (q >> 1)) + (q & 1);
-                if (col < wf) (*owner)[col] = b;
-            }
-        }
-    }
 }
 
 // the selected variant of length n, else variant 0
@@ -755,18 +726,6 @@ int fft_cols_ct_blocks(int height, int wf, int nbins) {
     return 0;
 }
 
-bool fft_cols_ct_owners(int height, int wf, int grid, std::vector<int>* owner) {
-    const int n_ = height;
-#define PHD_X(N, V, T, ...)                                  \
-    if (n_ == N && V == v_) {                                \
-        cols_owners<N, T, __VA_ARGS__>(wf, grid, owner);     \
-        return true;                                         \
-    }
-    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
-#undef PHD_X
-    return false;
-}
-
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
                               const double* k255, const double2* tw, double2* inter, hipStream_t st,
                               unsigned long long* rsum) {
@@ -797,7 +756,7 @@ hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int
                                     const unsigned long long* sums, long sums_stride, hipStream_t st) {
     // bin windows are made for one image's column owners (the batch spreads
     // each image's columns over other blocks)
-    if (n < 1 || (cb.win && n > 1)) return hipErrorInvalidValue;
+    if (n < 1) return hipErrorInvalidValue;
     const int n_ = height;
 #define PHD_X(N, V, T, ...)                                                                                    \
     if (n_ == N && V == v_)                                                                                    \

@@ -112,50 +112,6 @@ bool build_blur_table(int height, int width, int nr, int na, BlurTable* t) {
     return true;
 }
 
-bool build_col_windows(const BlurTable& t, int grid, const std::vector<int>& owner, ColWin* w) {
-    const int H = t.height, wf = t.wf, nr = t.nr;
-    std::vector<int> a0(grid, 1 << 30), a1(grid, -1), r0(grid, 1 << 30), r1(grid, -1);
-    for (int x = 0; x < wf; x++) {
-        const int b = owner[x];
-        if (b < 0 || b >= grid) return false;                // every column has one block
-        const uint16_t* col = t.map.data() + (size_t)x * H;
-        for (int u = 0; u < H; u++) {
-            const int pb = col[u] / nr, rb = col[u] - pb * nr;
-            a0[b] = std::min(a0[b], pb);
-            a1[b] = std::max(a1[b], pb);
-            r0[b] = std::min(r0[b], rb);
-            r1[b] = std::max(r1[b], rb);
-        }
-    }
-    std::vector<int> win(2 * (size_t)grid, 0);
-    int wmax = 1;
-    for (int b = 0; b < grid; b++) {
-        if (a1[b] < 0) continue;                             // a block without columns
-        win[2 * b] = a0[b] * nr + r0[b];
-        win[2 * b + 1] = r1[b] - r0[b] + 1;
-        wmax = std::max(wmax, (a1[b] - a0[b] + 1) * (r1[b] - r0[b] + 1));
-    }
-    if (wmax > 65535) return false;
-    w->lmap.assign(t.map.size(), 0);
-    for (int x = 0; x < wf; x++) {
-        const int b = owner[x];
-        const uint16_t* col = t.map.data() + (size_t)x * H;
-        uint16_t* lc = w->lmap.data() + (size_t)x * H;
-        for (int u = 0; u < H; u++) {
-            const int pb = col[u] / nr, rb = col[u] - pb * nr;
-            lc[u] = (uint16_t)((pb - a0[b]) * win[2 * b + 1] + (rb - r0[b]));
-        }
-    }
-    if (hipMalloc(&w->d_win, win.size() * sizeof(int)) != hipSuccess ||
-        hipMemcpy(w->d_win, win.data(), win.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
-        set_error("upload of the column bin windows failed");
-        return false;
-    }
-    w->grid = grid;
-    w->win_max = wmax;
-    return true;
-}
-
 bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r) {
     const int H = height, E = (H + T - 1) / T;
     std::vector<int> nrun(wf, 0);

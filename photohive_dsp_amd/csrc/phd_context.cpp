@@ -320,47 +320,6 @@ const double2* get_ct_twiddles(Context* c, int n, bool rows) {
     return d;
 }
 
-// The compile-time column pass's bin windows for a table: the grid the
-// kernel's occupancy gives with the windows' LDS and the windows made for that
-// grid must agree (a window is sized by the columns a block owns, the grid by
-// the largest window), so iterate from the bins-free grid.  nullptr when no
-// window set is consistent, or when the windows would not put more blocks on
-// a CU than the full table does (measured: at the same occupancy the full
-// table is the faster, 55.7 against 60.0 us at 4000x3000; 4000-row columns at
-// two blocks per CU instead of one, 103.6 against 143.3 us).
-int col_windows_mode(int set) {
-    static std::atomic<int> mode{phd_knob("PHD_COL_WINDOWS") ? atoi(phd_knob("PHD_COL_WINDOWS")) : 1};
-    return set >= 0 ? mode.exchange(set) : mode.load();
-}
-
-static ColWin* get_col_windows(Context* c, const BlurTable& t, int width) {
-    const int mode = col_windows_mode(-1);                  // 0 off, 1 where they raise occupancy, 2 always
-    if (mode == 0) return nullptr;
-    const int nbins = t.na * t.nr;
-    const int g_full = fft_cols_ct_blocks(t.height, t.wf, nbins);
-    int grid = fft_cols_ct_blocks(t.height, t.wf, 1);
-    if (mode == 1 && grid <= g_full) return nullptr;
-    for (int it = 0; it < 3; it++) {
-        const auto key = std::make_tuple(t.height, width, t.nr, t.na, grid);
-        auto f = c->colwins.find(key);
-        ColWin* w = nullptr;
-        if (f != c->colwins.end()) {
-            w = &f->second;
-        } else {
-            std::vector<int> owner;
-            ColWin cw;
-            if (!fft_cols_ct_owners(t.height, t.wf, grid, &owner) || !build_col_windows(t, grid, owner, &cw))
-                return nullptr;
-            w = &(c->colwins[key] = cw);
-        }
-        if (w->win_max >= nbins) return nullptr;
-        const int g2 = fft_cols_ct_blocks(t.height, t.wf, w->win_max);
-        if (g2 == grid) return (mode == 1 && grid <= g_full) ? nullptr : w;
-        grid = g2;
-    }
-    return nullptr;
-}
-
 // batch: the caller will run the compile-time passes as batched launches,
 // whose blocks take different columns of each image, so no per-block bin
 // windows (they are made for one image's column owners)
@@ -374,16 +333,13 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         if (reinterpret_cast<uintptr_t>(imgs[i]) & 3) ct = false;   // dword row loads
     // the column pass sums bins from per-column run lists (ColRuns); a table
     // with more than kColRunsMax runs in a column takes the runtime plans
-    ColWin* w = nullptr;
     const ColRuns* runs = nullptr;
     if (ct && tbl) {
+        // (round 4: the column pass sums its bins per run, so the per-block
+        // bin windows that once shrank its LDS bin array are not used)
         const int T = fft_cols_ct_threads(height);
-        w = batch ? nullptr : get_col_windows(c, *tbl, width);
-        if (w) {
-            if (w->runs.T == 0 && !build_col_runs(w->lmap.data(), tbl->height, tbl->wf, T, &w->runs)) w = nullptr;
-            else runs = &w->runs;
-        }
-        if (!runs) {
+        (void)batch;
+        {
             const auto key = std::make_tuple(height, width, tbl->nr, tbl->na, T);
             auto f = c->colruns.find(key);
             if (f == c->colruns.end()) {
@@ -399,14 +355,8 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         s->tw_r = get_ct_twiddles(c, width, true);
         s->tw_c = get_ct_twiddles(c, height, false);
         if (!s->tw_r || !s->tw_c) return false;
-        if (w) {
-            s->cbins = ColBins{runs->d_runs, runs->d_seg, runs->stride, w->d_win, w->win_max, tbl->nr, w->grid};
-            s->col_blocks = w->grid;
-        } else {
-            s->cbins = ColBins{runs ? runs->d_runs : nullptr, runs ? runs->d_seg : nullptr, runs ? runs->stride : 0,
-                               nullptr, nbins, tbl ? tbl->nr : 0, 0};
-            s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
-        }
+        s->cbins = ColBins{runs ? runs->d_runs : nullptr, runs ? runs->d_seg : nullptr, runs ? runs->stride : 0};
+        s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
         return true;
     }
     if (!gfft_direct_ok(width) || !gfft_direct_ok(height)) return select_generic(c, height, width, nbins, s);

@@ -83,24 +83,12 @@ struct ColRuns {
     uint32_t* d_runs = nullptr;          // device [wf][stride]
     uint8_t* d_seg = nullptr;            // device [wf][T]
 };
-// The compile-time column pass's per-block polar-bin windows for one table
-// and grid (ColBins, phd_internal.h): window-local bin ids, each block's first
-// bin and radius width, the largest window.
-struct ColWin {
-    int grid = 0, win_max = 0;
-    std::vector<uint16_t> lmap;          // host [wf][height] window-local bin ids (the runs are made from it)
-    int* d_win = nullptr;                // device [grid][2]
-    ColRuns runs;                        // lmap's runs (T = 0: not built yet)
-};
 // false when a column needs more than kColRunsMax entries (that size then
 // takes the runtime-plan FFT) or on an upload error.
 bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r);
 // Exact (phi_bin, r_bin) of every spectrum element, glibc atan2 + newton_int_sqrt
 // exactly as src/blur_profile.c:87-97 / 427-458.
 bool build_blur_table(int height, int width, int nr, int na, BlurTable* t);
-// The per-block windows of the column pass for `grid` blocks (owner[col] =
-// the block of each column): false when a window would not be smaller.
-bool build_col_windows(const BlurTable& t, int grid, const std::vector<int>& owner, ColWin* w);
 void vectorize_blur(const double* bins, int na, int nr, double streak, double mag, int denom,
                     Blur_Vector* out10);
 
@@ -181,7 +169,6 @@ struct Context {
     std::map<std::pair<int, bool>, FftPlanHost> plans;   // (length, composite)
     std::map<std::pair<int, int>, double2*> ct_tw;  // (length, rows?) -> compile-time plan twiddles
     std::map<std::tuple<int, int, int, int>, BlurTable> tables;
-    std::map<std::tuple<int, int, int, int, int>, ColWin> colwins;   // (H, W, nr, na, grid)
     std::map<std::tuple<int, int, int, int, int>, ColRuns> colruns;  // (H, W, nr, na, T): full-table runs
     std::map<int, GfftPlan> gplans;                 // global-memory FFT plans by length
     double2* d_gbuf = nullptr;                      // generic 2-D path: row pairs + scratch

@@ -321,6 +321,10 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(3000, 13, 256, 1, 15, 10, 20)    \
     X(3000, 14, 256, 1, 10, 15, 20)    \
     X(3000, 15, 256, 5, 10, 15, 20)    \
+    X(3000, 16, 256, 69, 15, 10, 20)   \
+    X(3000, 17, 256, 69, 15, 20, 10)   \
+    X(3000, 18, 256, 69, 10, 15, 20)   \
+    X(3000, 19, 256, 69, 25, 12, 10)   \
     X(6000, 0, 512, 5, 15, 20, 20)     \
     X(6000, 1, 512, 5, 10, 20, 30)     \
     X(4000, 0, 256, 5, 10, 20, 20)     \
@@ -360,28 +364,18 @@ inline size_t inter_elems(int height, int width) {
 }
 constexpr int kColRunsMax = 256;   // entries (runs + sentinel) of one column's list (LDS)
 struct ColBins {
-    const uint32_t* runs = nullptr;  // [wf][rstride] runs of one bin id (ColRuns, phd_host.h): global ids
-                                     // (win == nullptr) or window-local
+    const uint32_t* runs = nullptr;  // [wf][rstride] runs of one polar bin (ColRuns, phd_host.h)
     const uint8_t* seg = nullptr;    // [wf][T] the run holding each thread's first row
     int rstride = 0;                 // entries per column
-    const int* win = nullptr;        // [grid][2] {global id of the window's first bin, window radius width}
-    int nlb = 0;                     // LDS bins: na * nr, or the largest window
-    int nr = 0;                      // radius_partitions (window decode)
-    int grid = 0;                    // the grid the windows were made for (0: from occupancy)
 };
 size_t fft_cols_ct_lds(int height, int nlb);
 // threads per column of the compile-time column plan for a height (0: none)
 int fft_cols_ct_threads(int height);
 // log_mant (phd_device.h) over n positive doubles (tests)
 hipError_t launch_log_mant(const double* x, double* y, long n, hipStream_t st);
-// the column-pass bin windows: 0 off, 1 where they raise occupancy (default),
-// 2 always; -1 leaves PHD_COL_WINDOWS / the default (phd_debug_col_windows)
-int col_windows_mode(int set);
-// persistent grid of the column kernel (= entries of fmax_part) with nlb LDS bins
+// persistent grid of the column kernel (= entries of fmax_part); nlb unused
+// since the bins are summed per run (round 4)
 int fft_cols_ct_blocks(int height, int wf, int nlb);
-// the block that processes each column (owner[col]) under the column kernel's
-// schedule for a grid of `grid` blocks (false: no compile-time plan)
-bool fft_cols_ct_owners(int height, int wf, int grid, std::vector<int>* owner);
 // tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built).
 // The row pass transforms the luma as is (sums unused): it does not wait for K1.
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,

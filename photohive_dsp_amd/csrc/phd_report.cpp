@@ -532,7 +532,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     static const bool gbatch_off = phd_knob("PHD_FFT_NO_BATCH") != nullptr;
     const bool gbatch = !fs.ct && !fs.generic && !gbatch_off && n > 1 && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
     if (gbatch) Q = std::max(1, std::min(n, (int)(((size_t)128 << 20) / inter_one)));
-    const bool ctbatch = fs.ct && ct_batchable && !fs.cbins.win && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
+    const bool ctbatch = fs.ct && ct_batchable && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
     if (ctbatch) Q = q_ct;
     const bool pipe = !gbatch && !ctbatch && !fs.generic && Q == 1 && n > 1 && pipe_env;
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
@@ -1758,7 +1758,6 @@ extern "C" int phd_debug_log_mant(const double* d_x, double* d_y, long n) {
     return 0;
 }
 
-extern "C" int phd_debug_col_windows(int mode) { return col_windows_mode(mode); }
 
 extern "C" int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int width, double* d_out) {
     clear_error();

@@ -37,28 +37,6 @@ def test_log_mant_matches_host_log():
     assert err.max() <= 4e-16, (err.max(), x[np.argmax(err)])
 
 
-@pytest.mark.parametrize("shape", [(4000, 6000), (3000, 4000)])
-def test_column_bin_windows_bit_identical(shape):
-    """The per-block LDS windows of polar bins sum the same fixed-point run values
-    into the same bins as the full table: bins and vectors bit-identical with the
-    windows off, where the occupancy rule turns them on (4000-row columns) and
-    forced (3000-row columns)."""
-    L, torch = _lib()
-    from photohive_dsp_amd import synth
-    from photohive_dsp_amd.core import blur_profiles_device
-    h, w = shape
-    imgs = torch.from_numpy(np.stack([synth.make("structured", h, w, 21), synth.uniform(h, w, 22)])).cuda()
-    prev = L.lib.phd_debug_col_windows(0)
-    try:
-        off_bins, off_vecs = blur_profiles_device(imgs)
-        L.lib.phd_debug_col_windows(2)
-        on_bins, on_vecs = blur_profiles_device(imgs)
-    finally:
-        L.lib.phd_debug_col_windows(prev)
-    assert np.array_equal(on_bins, off_bins)
-    assert on_vecs == off_vecs
-
-
 def test_mixed_batch_groups_past_64_images():
     """phd_report_batch_device_mixed runs small sizes in groups larger than 64
     (pixel budget, phd_report.cpp size_groups): 70 images of 352x352 between
