@@ -754,8 +754,6 @@ hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int
                                     const ColBins& cb, unsigned long long* bin_sums, long bin_stride,
                                     double* fmax_part, long fmax_stride, const double2* tw,
                                     const unsigned long long* sums, long sums_stride, hipStream_t st) {
-    // bin windows are made for one image's column owners (the batch spreads
-    // each image's columns over other blocks)
     if (n < 1) return hipErrorInvalidValue;
     const int n_ = height;
 #define PHD_X(N, V, T, ...)                                                                                    \

@@ -320,9 +320,8 @@ const double2* get_ct_twiddles(Context* c, int n, bool rows) {
     return d;
 }
 
-// batch: the caller will run the compile-time passes as batched launches,
-// whose blocks take different columns of each image, so no per-block bin
-// windows (they are made for one image's column owners)
+// batch: the caller will run the compile-time passes as batched launches
+// (one row and one column launch per group of same-size images)
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
                 const BlurTable* tbl, bool batch) {
     *s = FftSel{};

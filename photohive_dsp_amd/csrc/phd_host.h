@@ -67,7 +67,7 @@ bool decide_palette(const GridParams& gp, const GroupCenters& gc, const unsigned
 struct BlurTable {
     int height = 0, wf = 0, nr = 0, na = 0;
     std::vector<long long> counts;       // [na*nr]
-    std::vector<uint16_t> map;           // host [wf][height] (the column windows are made from it)
+    std::vector<uint16_t> map;           // host [wf][height] (the column run lists are made from it)
     uint16_t* d_map = nullptr;           // device [wf][height]
     int angle_bin_size = 0, radius_bin_size = 0;
 };
@@ -288,7 +288,7 @@ struct FftSel {
     const double2* tw_r = nullptr;
     const double2* tw_c = nullptr;
     int col_blocks = 0;   // entries of the per-block max partials
-    ColBins cbins;        // compile-time column pass: the bins it sums into (windows or the full table)
+    ColBins cbins;        // compile-time column pass: its per-column polar-bin runs
     // the generic path (a side above the LDS limit or with a large prime
     // factor): row pairs -> global row transforms -> split / transpose, then
     // the fused runtime column pass (cols_fused) or global column transforms
@@ -298,8 +298,8 @@ struct FftSel {
     const GfftPlan* gcol = nullptr;
     double2* gbuf = nullptr;
 };
-// tbl: the polar-bin table of the size (the compile-time column pass's bin
-// windows are made from it; nullptr: every block sums all na * nr bins)
+// tbl: the polar-bin table of the size (the compile-time column pass's run
+// lists are made from it; nullptr: no compile-time column pass can launch)
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
                 const BlurTable* tbl, bool batch = false);
 hipError_t launch_rows_sel(const FftSel& s, const uint8_t* img, int height, int width,

@@ -342,12 +342,9 @@ int ct_variant(bool rows);
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);
 bool ct_cols_plan(int h, std::vector<int>* radices);
-// The polar bins the compile-time column pass sums into.  Each block's
-// columns touch a rectangle of (angle, radius) bins, so a block can sum into an
-// LDS window of that rectangle (window-local ids in `map`, decoded through
-// `win` when the block adds its window to the image's bins) instead of all
-// na * nr bins: 1.1-14 KB instead of 23 KB of LDS at 72 x 40 bins, which lets
-// two column blocks share a CU where the full table did not fit beside them.
+// The polar bins the compile-time column pass sums into, as per-column run
+// lists (round 4; the round-3 per-block LDS windows of bins are gone: the pass
+// sums each run in an LDS slot and adds the slots to the image's bins).
 // The compile-time FFT passes' half-spectrum intermediate (fft_ct.hip): row
 // pair p's tile row of 4 KP elements (KP = ceil((W/2+1) / 2) column pairs,
 // 16 B each) starts at p * ct_row_stride(W), a multiple of 8 elements, so every
