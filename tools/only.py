@@ -21,11 +21,11 @@ def main():
     cx = bench.Ctx(args, 1, 0, "nccl")
     cx.lib.phd_set_lanes(int(os.environ.get("ONLY_LANES", "1")))
     for leg in legs:
-        if leg == "headline":
-            hl = bench.headline(cx)
+        if leg in ("headline", "structured"):
+            hl = bench.headline(cx, kind="hblur" if leg == "structured" else "uniform")
             m = hl["merged"]
             out = {"images_per_s": round(m["images"] / m["elapsed"], 1),
-                   "ms_per_step": round(1000 * m["elapsed"] / args.steps, 3),
+                   "ms_per_step": round(1000 * m["elapsed"] / hl["steps"], 3),
                    "dom": hl["dom"], "warm_us": {k: round(v["avg_us"], 2) for k, v in hl["warm"].items()},
                    "stages": {k: round(v, 3) for k, v in hl["stages"].items()}}
         elif leg == "config3":
