@@ -45,15 +45,13 @@ def parse(argv=None):
                    help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64, "
                         "7.0-7.3k at 128, 7.4k at 256 on one box (round 3): the per-call fixed costs -- K1's "
                         "prologue and tail, the host head and tail of a call -- amortised; 9.2 GB of pixels)")
-    p.add_argument("--lanes", type=int, default=1,
-                   help="library lanes for every config of the run (phd_set_lanes; the library's default is 1): "
-                        "1 keeps each kernel launch alone on the GPU, so its event duration prices the kernel "
-                        "(the roofline)")
-    p.add_argument("--two-lanes", action="store_true",
-                   help="also run the headline workload over two library lanes (phd_set_lanes(2), the opt-in "
-                        "concurrent mode) and report its images/s as two_lanes; off by default so that every "
-                        "kernel launch of the default command runs alone and its rocprofv3 statistics agree "
-                        "with the roofline")
+    p.add_argument("--lanes", type=int, default=2,
+                   help="library lanes for every config of the run (phd_set_lanes; 2 is the library's default: "
+                        "each call split into two concurrent halves, +10-13 %% images/s over 1).  With 2 the "
+                        "headline roofline is the whole pipeline's and one_lane repeats the headline on one "
+                        "lane, where each launch of the dominant kernel runs alone and its events price it")
+    p.add_argument("--no-one-lane", action="store_true",
+                   help="skip the one-lane repeat of the headline (one_lane)")
     p.add_argument("--height", type=int, default=3000)
     p.add_argument("--width", type=int, default=4000)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -299,6 +297,74 @@ def pipeline_roofline(images_per_s, H, W):
             "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_image": algorithmic_bytes("report", H, W)}
 
 
+def pmc_traffic(args, H, W):
+    """The per-kernel HBM bytes of the committed PMC passes (tools/pmc_collect.py)
+    for this image size, with where they come from; (None, None) without them."""
+    try:
+        with open(args.pmc) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if pm.get("image") != f"{H}x{W}" or not pm.get("kernels"):
+        return None, None
+    src = (f"{os.path.relpath(args.pmc, ROOT)}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
+           "config (tools/pmc_collect.py), not measured in this run")
+    if pm.get("calibration"):
+        src += f"; FETCH_SIZE x each kernel's fetch_factor, calibrated on its algorithmic bytes ({pm['calibration']})"
+    return pm["kernels"], src
+
+
+def dominant_roofline(hl, args):
+    """The dominant kernel against HBM: its algorithmic bytes per launch over its
+    average launch duration, from the HIP events of the timed region (every
+    launch of every 4th step, all ranks; one lane, so each launch runs alone)."""
+    H, W, B = args.height, args.width, args.batch
+    m, dom, warm, kern = hl["merged"], hl["dom"], hl["warm"], hl["kern"]
+    if dom not in kern:
+        return None
+    # the palette passes take the whole batch in one launch, the FFT passes one image
+    per_launch = hl["warm_steps"] * B / warm[dom]["launches"]
+    ab = algorithmic_bytes(dom, H, W) * per_launch
+    avg_us = 1000 * m["kernel_ms"] / max(m["launches"], 1)      # all ranks' sampled launches
+    achieved = ab / (avg_us * 1e-6) / 1e9
+    kt, tsrc = pmc_traffic(args, H, W)
+    traffic = kt[dom]["hbm_bytes_per_image"] * per_launch if kt and dom in kt else None
+    return {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": tsrc if traffic else None, "algorithmic_bytes_per_launch": ab,
+            "images_per_launch": per_launch, "avg_launch_us": round(avg_us, 2), "launches_timed": int(m["launches"]),
+            "sampling": "every launch of every 4th timed step, all ranks"}
+
+
+def pipeline_headline_roofline(value, hl, args):
+    """Two lanes: the launches of the two halves overlap, so no one kernel's
+    duration prices it; the headline roofline is the whole report's --
+    SURVEY.md 8(d)'s 9 N + 32 H Wf bytes per image x the timed region's images/s
+    (its wall clock, all ranks) -- with the PMC bytes of every kernel of the
+    report summed per image as traffic.  dominant_kernel_shared: the column
+    pass's events in a two-lane warm-up step (shared launches); one_lane.roofline
+    has it alone."""
+    H, W, B = args.height, args.width, args.batch
+    out = pipeline_roofline(value, H, W)
+    out = {"kernel": "report pipeline (hsv_stats + fft_rows + fft_cols + palette passes, two lanes)", **out}
+    kt, tsrc = pmc_traffic(args, H, W)
+    if kt:
+        out["traffic"] = round(sum(v["hbm_bytes_per_image"] for v in kt.values()))
+        out["traffic_source"] = tsrc + f"; summed over {sorted(kt)} per image"
+        out["traffic_per"] = "image"
+    else:
+        out["traffic"] = None
+    out["basis"] = "images/s of the timed region x algorithmic bytes per image"
+    dom, warm = hl["dom"], hl["warm"]
+    if dom in warm:
+        per_launch = B / warm[dom]["launches"]
+        gbs = algorithmic_bytes(dom, H, W) * per_launch / (warm[dom]["avg_us"] * 1e-6) / 1e9
+        out["dominant_kernel_shared"] = {"kernel": dom, "avg_launch_us": round(warm[dom]["avg_us"], 2),
+                                         "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                         "source": "HIP events on every launch of one two-lane warm-up step"}
+    return out
+
+
 class Ctx:
     """Per-rank state shared by the configs."""
 
@@ -372,19 +438,37 @@ def headline(cx, timed_events=True, kind="uniform", steps=None):
     # The candidates are the three per-image passes (the palette tail runs once
     # per step, ~0.2 ms); the last warmup steps are the profiled ones.
     cand = [] if args.no_kernel_events else ["fft_cols", "fft_rows", "hsv_stats"][:max(1, args.warmup)]
+    lanes = lib.phd_set_lanes(0)
     lib.phd_profile_kernels(0)
     for _ in range(max(1, args.warmup) - len(cand)):
         step()
-    warm = {}
-    for name in cand:
-        lib.phd_profile_kernels(1 << KERNELS.index(name))
+
+    def time_candidates():
+        out = {}
+        for name in cand:
+            lib.phd_profile_kernels(1 << KERNELS.index(name))
+            step()
+            out.update({n: v for n, v in kernel_times(lib, KERNELS).items() if n == name})
+        lib.phd_profile_kernels(0)
+        return out
+    warm = time_candidates()
+    # with two lanes each launch shares the GPU with the other lane's: the same
+    # candidates once more on one lane price each kernel alone (per_kernel)
+    warm_alone = warm
+    if lanes > 1 and cand:
+        lib.phd_set_lanes(1)
+        warm_alone = time_candidates()
+        lib.phd_set_lanes(lanes)
         step()
-        warm.update({n: v for n, v in kernel_times(lib, KERNELS).items() if n == name})
     nprof = 1
     dom = max(warm, key=lambda k: warm[k]["total_ms"]) if warm else None
-    # timed region: HIP events (recorded by the launches themselves, on the
-    # stream the kernel runs on) bracket every launch of the dominant kernel in
-    # every 4th step
+    # timed region, one lane: HIP events (recorded by the launches themselves,
+    # on the stream the kernel runs on) bracket every launch of the dominant
+    # kernel in every 4th step.  Two lanes: none (they cost ~3 % of the
+    # throughput there; the headline roofline is then the pipeline's, priced on
+    # the timed region's wall clock)
+    if lanes > 1:
+        timed_events = False
     lib.phd_profile_kernels(0 if dom is None or not timed_events else (1 << KERNELS.index(dom)) | (4 << 24))
     cx.barrier()
     t0 = time.perf_counter()
@@ -405,7 +489,8 @@ def headline(cx, timed_events=True, kind="uniform", steps=None):
     m = cx.merge(elapsed, n_img, n_img * H * W, n_img * algorithmic_bytes("report", H, W), km, kl)
     del d_imgs
     torch.cuda.empty_cache()
-    res = {"merged": m, "dom": dom, "warm": warm, "warm_steps": nprof, "kern": kern, "steps": steps,
+    res = {"merged": m, "dom": dom, "warm": warm, "warm_alone": warm_alone, "warm_steps": nprof, "kern": kern,
+           "steps": steps, "lanes": lanes,
            "stages": {k: stage[j] / steps for j, k in enumerate(
                ("hsv_stats", "fft_rows_cols", "palette_pass2", "gpu_total", "host_total", "host_enqueue",
                 "host_decisions", "host_assembly"))}}
@@ -772,25 +857,20 @@ def main(argv=None):
     cx.lib.phd_set_lanes(args.lanes)                  # every config of this run
     hl = headline(cx)
     extra = {}
-    if args.two_lanes and args.lanes == 1:
-        # the same workload split over two library lanes (concurrent halves):
-        # more images/s, but each launch now shares the GPU, so its duration no
-        # longer prices the kernel alone
-        cx.lib.phd_set_lanes(2)
-        # (no kernel events in its timed region: with two lanes they cost ~10 %;
-        # the shared launch duration comes from the warm-up step that times the
-        # dominant kernel)
-        h2 = headline(cx, timed_events=False)
+    if hl["lanes"] > 1 and not args.no_one_lane:
+        # the same workload on one lane: each launch alone on the GPU, so the
+        # events in its timed region price the dominant kernel (the roofline of
+        # the driver's contract); the headline's two lanes share the GPU
+        cx.lib.phd_set_lanes(1)
+        h1 = headline(cx)
         cx.lib.phd_set_lanes(args.lanes)
-        m2 = h2["merged"]
-        w2 = h2["warm"].get(h2["dom"], {})
-        extra["two_lanes"] = {
-            "workload": f"as the headline, each {args.batch}-image call split over 2 library lanes "
-                        "(phd_set_lanes(2): two contexts, the second on a library thread)",
-            "images_per_s": round(m2["images"] / m2["elapsed"], 1),
-            "ms_per_step": round(1000 * m2["elapsed"] / args.steps, 3),
-            "dominant_kernel": h2["dom"],
-            "avg_launch_us_shared_warmup": round(w2.get("avg_us", 0.0), 2)}
+        if rank == 0:
+            m1 = h1["merged"]
+            extra["one_lane"] = {
+                "workload": f"as the headline, each {args.batch}-image call on one library lane (phd_set_lanes(1))",
+                "images_per_s": round(m1["images"] / m1["elapsed"], 1),
+                "ms_per_step": round(1000 * m1["elapsed"] / h1["steps"], 3),
+                "roofline": dominant_roofline(h1, args)}
     if not args.no_configs:
         # the same workload on structured images
         hs = headline(cx, timed_events=False, kind="hblur", steps=max(5, args.steps // 5))
@@ -799,10 +879,10 @@ def main(argv=None):
         extra["config2_structured"] = {
             "workload": f"full report, {args.height}x{args.width} RGB8 structured (synth.py hblur: gradient + disks "
                         f"+ 15-px horizontal box blur, generated on the device, seed 2 + image index), batch "
-                        f"{args.batch}/GPU, device-resident",
+                        f"{args.batch}/GPU, {hs['lanes']} library lane(s), device-resident",
             "images_per_s": round(ips, 1), "ms_per_step": round(1000 * ms["elapsed"] / hs["steps"], 3),
             "steps": hs["steps"], "stages_ms_per_step_rank0": hs["stages"],
-            "per_kernel": per_kernel_roofline(hs["warm"], args.batch, args.height, args.width),
+            "per_kernel": per_kernel_roofline(hs["warm_alone"], args.batch, args.height, args.width),
             "roofline_pipeline": pipeline_roofline(ips, args.height, args.width)}
         extra["config4"] = config4(cx, args.config4_images)
         extra["config5"] = config5(cx, args.config5_images)
@@ -832,44 +912,19 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (device splitmix64 uniform RGB8)",
-            "config": {"workload": f"full report, {H}x{W} RGB8, batch {B}/GPU, device-resident",
+            "config": {"workload": f"full report, {H}x{W} RGB8, batch {B}/GPU, {hl['lanes']} library lane(s), "
+                                   "device-resident",
                        "global_batch": B * world, "image": f"{H}x{W}",
                        "parallelism": f"images sharded over {world} GPU"},
             "hbm_GB_per_s_algorithmic": round(m["alg_bytes"] / m["elapsed"] / 1e9, 1),
             "stages_ms_per_step_rank0": hl["stages"],
         }
-        dom, warm, kern = hl["dom"], hl["warm"], hl["kern"]
-        line["roofline"] = None
-        if dom in kern:
-            # the palette passes take the whole batch in one launch, the FFT passes one image
-            # (from the last warmup step, whose every launch was bracketed)
-            per_launch = hl["warm_steps"] * B / warm[dom]["launches"]
-            ab = algorithmic_bytes(dom, H, W) * per_launch
-            # every rank's sampled launches of the dominant kernel (counter all-gather)
-            avg_us = 1000 * m["kernel_ms"] / max(m["launches"], 1)
-            achieved = ab / (avg_us * 1e-6) / 1e9
-            traffic, tsrc = None, None
-            try:
-                with open(args.pmc) as f:
-                    pm = json.load(f)
-                if pm.get("image") == f"{H}x{W}" and dom in pm.get("kernels", {}):
-                    traffic = pm["kernels"][dom]["hbm_bytes_per_image"] * per_launch
-                    tsrc = (f"{os.path.relpath(args.pmc, ROOT)}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                            "passes of this config (tools/pmc_collect.py), not measured in this run")
-                    if pm.get("calibration"):
-                        f = pm["kernels"][dom].get("fetch_factor")
-                        tsrc += (f"; FETCH_SIZE x {f:.3f} for this kernel's access pattern, calibrated on its "
-                                 f"algorithmic bytes ({pm['calibration']})")
-            except (OSError, ValueError, KeyError):
-                pass
-            line["roofline"] = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 1),
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                                "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes_per_launch": ab,
-                                "images_per_launch": per_launch, "avg_launch_us": round(avg_us, 2),
-                                "launches_timed": int(m["launches"]),
-                                "sampling": "every launch of every 4th timed step, all ranks"}
-            line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in warm.items()}
-        line["per_kernel"] = per_kernel_roofline(warm, B, H, W)
+        if hl["lanes"] > 1:
+            line["roofline"] = pipeline_headline_roofline(value, hl, args)
+        else:
+            line["roofline"] = dominant_roofline(hl, args)
+        line["warmup_kernels_us_per_launch"] = {k: round(v["avg_us"], 2) for k, v in hl["warm"].items()}
+        line["per_kernel"] = per_kernel_roofline(hl["warm_alone"], B, H, W)
         line["roofline_pipeline"] = pipeline_roofline(value, H, W)
         line.update(extra)
         line["vs_baseline_note"] = ("null: BASELINE.md publishes no number for this metric (its only figures are "

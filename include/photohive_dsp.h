@@ -272,10 +272,11 @@ int phd_profile_kernels(unsigned mask);
 int phd_profile_read(int kernel, double* total_ms, long* launches);
 
 /* Lanes a device batch of >= 16 images on the library's stream is split over
- * (1 or 2; default 1, or PHD_LANES).  Each lane is an independent context with
+ * (1 or 2; default 2, or PHD_LANES).  Each lane is an independent context with
  * its own streams and workspaces; the second runs on a library thread, so the
- * two halves' kernels, host phases and launch gaps overlap (+8-11 % images/s at
- * 4000x3000, bench.py's two_lanes object).  Results do not depend on it.  With
+ * two halves' kernels, host phases and launch gaps overlap (+10-13 % images/s
+ * at 4000x3000 over one lane, bench.py's one_lane object).  Results do not
+ * depend on it.  With
  * two lanes, phd_last_timings and PHD_VERBOSE's stage lines cover lane 0's half
  * of a batch only (the stage timings are per calling thread).  lanes < 1 only
  * queries.  Returns the previous setting. */

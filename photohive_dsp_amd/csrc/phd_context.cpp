@@ -153,9 +153,9 @@ int lanes_setting() {
     int l = g_lanes.load();
     if (l < 0) {
         const char* e = getenv("PHD_LANES");
-        // one lane unless asked for: the default is what bench.py's headline and
-        // roofline measure (each kernel launch alone on the GPU)
-        l = e ? std::min(std::max(atoi(e), 1), kLanes) : 1;
+        // two lanes unless asked for: each large call split into two concurrent
+        // halves (+10-13 % images/s at 4000x3000, DESIGN.md "Lanes")
+        l = e ? std::min(std::max(atoi(e), 1), kLanes) : 2;
         g_lanes.store(l);
     }
     return l;

@@ -124,6 +124,22 @@ def test_reference_rejections_are_null_before_touching_gpu():
         assert "350" in last_error() or "aspect" in last_error()
 
 
+def test_lanes_default_is_two_and_phd_lanes_overrides():
+    """The library's default is two lanes (phd_context.cpp lanes_setting);
+    PHD_LANES=1 selects one (a fresh process each: the setting is read once)."""
+    import subprocess
+    import sys
+    code = "from photohive_dsp_amd.lib import lib; print(lib.phd_set_lanes(0))"
+    for env_val, want in ((None, 2), ("1", 1), ("2", 2)):
+        env = {k: v for k, v in os.environ.items() if k != "PHD_LANES"}
+        if env_val is not None:
+            env["PHD_LANES"] = env_val
+        out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, out.stderr
+        assert int(out.stdout.strip().splitlines()[-1]) == want
+
+
 def test_lanes_setting_and_batch_free_need_no_gpu():
     """phd_set_lanes clamps to 1..2 and lanes < 1 only query; phd_free_reports
     skips NULL entries and leaves every entry NULL (host-only calls)."""

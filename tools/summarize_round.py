@@ -1,5 +1,4 @@
-"""Print the key figures of a profiling round (run after tools/prof_round.sh
-and, optionally, bench.py --two-lanes > gpurun_out/bench_two_lanes.log)."""
+"""Print the key figures of a profiling round (run after tools/prof_round.sh)."""
 import csv
 import json
 import os
@@ -17,14 +16,14 @@ def last_json(path):
 def main():
     d = last_json(os.path.join(OUT, "bench_full.log"))
     r = d["roofline"]
-    print("headline", d["value"], r["kernel"], r["avg_launch_us"], r["frac"])
+    print("headline", d["value"], r["kernel"], r["frac"], r.get("dominant_kernel_shared"))
+    if "one_lane" in d:
+        o = d["one_lane"]
+        print("one_lane", o["images_per_s"], o["roofline"]["kernel"], o["roofline"]["avg_launch_us"],
+              o["roofline"]["frac"])
     print("config4", d["config4"]["images_per_s"], "config5", d["config5"]["images_per_s"])
     print("host_buffer", d["host_buffer"])
     print("config3 frac", d["config3"]["roofline"]["frac"], "single", d["config2_single"])
-    p = os.path.join(OUT, "bench_two_lanes.log")
-    if os.path.exists(p):
-        t = last_json(p)
-        print("two_lanes", t["value"], t["two_lanes"]["images_per_s"])
     for f in ("prof2", "prof"):
         path = os.path.join(OUT, f, "prof_kernel_stats.csv")
         if not os.path.exists(path):
