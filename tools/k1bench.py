@@ -9,6 +9,8 @@ from photohive_dsp_amd.lib import lib, last_error
 from photohive_dsp_amd.core import make_config
 from photohive_dsp_amd.structures import Full_Report_Data, RGB_Statistics
 
+lib.phd_set_lanes(1)              # each K1 launch alone on the GPU (the library's default is 2)
+
 
 KIND = os.environ.get("K1KIND", "uniform")          # or hblur: SURVEY 8(d) row 2(b)'s structured images
 

@@ -33,7 +33,7 @@ def short(name):
 
 def run_pass(counter, outdir, bench_args):
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
-           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-kernel-events"] + bench_args
+           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-kernel-events", "--lanes", "1"] + bench_args
     subprocess.run(cmd, check=True, cwd=ROOT)
     files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
     if not files:
