@@ -50,6 +50,10 @@ def parse(argv=None):
                         "each call split into two concurrent halves, +10-13 %% images/s over 1).  With 2 the "
                         "headline roofline is the whole pipeline's and one_lane repeats the headline on one "
                         "lane, where each launch of the dominant kernel runs alone and its events price it")
+    p.add_argument("--hw-queues", type=int, default=8,
+                   help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; 0 keeps the environment's): "
+                        "two lanes use 8 HIP streams, and with HIP's default of 4 hardware queues pairs of them share "
+                        "a queue and serialise (round 4: 8.32k images/s with 4, 8.81k with 8)")
     p.add_argument("--no-one-lane", action="store_true",
                    help="skip the one-lane repeat of the headline (one_lane)")
     p.add_argument("--height", type=int, default=3000)
@@ -337,16 +341,17 @@ def dominant_roofline(hl, args):
 
 
 def pipeline_headline_roofline(value, hl, args):
-    """Two lanes: the launches of the two halves overlap, so no one kernel's
+    """Two or more lanes: the launches of the lanes overlap, so no one kernel's
     duration prices it; the headline roofline is the whole report's --
     SURVEY.md 8(d)'s 9 N + 32 H Wf bytes per image x the timed region's images/s
     (its wall clock, all ranks) -- with the PMC bytes of every kernel of the
     report summed per image as traffic.  dominant_kernel_shared: the column
-    pass's events in a two-lane warm-up step (shared launches); one_lane.roofline
+    pass's events in a warm-up step on those lanes (shared launches); one_lane.roofline
     has it alone."""
     H, W, B = args.height, args.width, args.batch
     out = pipeline_roofline(value, H, W)
-    out = {"kernel": "report pipeline (hsv_stats + fft_rows + fft_cols + palette passes, two lanes)", **out}
+    out = {"kernel": f"report pipeline (hsv_stats + fft_rows + fft_cols + palette passes, {hl['lanes']} lanes)",
+           **out}
     kt, tsrc = pmc_traffic(args, H, W)
     if kt:
         out["traffic"] = round(sum(v["hbm_bytes_per_image"] for v in kt.values()))
@@ -361,7 +366,7 @@ def pipeline_headline_roofline(value, hl, args):
         gbs = algorithmic_bytes(dom, H, W) * per_launch / (warm[dom]["avg_us"] * 1e-6) / 1e9
         out["dominant_kernel_shared"] = {"kernel": dom, "avg_launch_us": round(warm[dom]["avg_us"], 2),
                                          "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                         "source": "HIP events on every launch of one two-lane warm-up step"}
+                                         "source": "HIP events on every launch of one warm-up step on the same lanes"}
     return out
 
 
@@ -824,6 +829,10 @@ def plan_only(args, world, rank):
 
 def main(argv=None):
     args = parse(argv)
+    if args.hw_queues > 0:
+        # read by HIP when it initialises: before this process (or the ranks
+        # spawn_ranks starts) makes any GPU call
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))

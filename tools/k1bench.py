@@ -31,8 +31,8 @@ def k1_avg():
     return 1000 * tot.value / max(cnt.value, 1)
 
 
-tag = os.environ.get("PHD_LIB", "default").split("/")[-1] + f" {KIND}" + (f" form {os.environ['PHD_K1_FORM']}" if os.environ.get("PHD_K1_FORM") else "")
-for n, h, w in [(64, 1080, 1920), (512, 1080, 1920)]:
+tag = os.environ.get("PHD_LIB", "default").split("/")[-1] + f" {KIND}" + (f" grid {os.environ['K1GRID']}" if os.environ.get("K1GRID") else "") + (f" form {os.environ['PHD_K1_FORM']}" if os.environ.get("PHD_K1_FORM") else "")
+for n, h, w in ([] if os.environ.get("K1ONLY") else [(64, 1080, 1920), (512, 1080, 1920)]):
     t = fill(n, h, w)
     st = (RGB_Statistics * n)()
     sat = (ctypes.c_double * n)()
@@ -48,7 +48,9 @@ for n, h, w in [(64, 1080, 1920), (512, 1080, 1920)]:
     del t
 n, h, w = int(os.environ.get("K1N", "64")), 3000, 4000
 t = fill(n, h, w)
-cfg = make_config()
+# K1GRID="36,4,5": config 5's finer palette grid (h/s/v partitions)
+grid = [int(x) for x in os.environ.get("K1GRID", "").split(",") if x]
+cfg = make_config(h_partitions=grid[0], s_partitions=grid[1], v_partitions=grid[2]) if grid else make_config()
 outs = (ctypes.POINTER(Full_Report_Data) * n)()
 stt = (ctypes.c_int * n)()
 lib.phd_profile_kernels(0)

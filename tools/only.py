@@ -15,6 +15,7 @@ def main():
     legs = sys.argv[1:] or ["config3"]
     args = bench.parse(["--steps", os.environ.get("ONLY_STEPS", "30"), "--warmup", "4",
                         "--batch", os.environ.get("ONLY_BATCH", "64")])
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", str(args.hw_queues))   # as bench.main, before HIP starts
     import torch
     torch.cuda.set_device(0)
     import photohive_dsp_amd  # noqa: F401
