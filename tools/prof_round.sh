@@ -16,8 +16,8 @@ for s in $STEPS; do
     k1) args+=("k1bench:200:python -u tools/k1bench.py");;
     calib) args+=("pmc_calib:400:python tools/pmc_calib.py");;
     pmc) args+=("pmc_collect:400:python tools/pmc_collect.py --tag $TAG -- --steps 3 --warmup 1 --no-configs --batch 8");;
-    prof) args+=("prof_config2:400:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof2 -o prof -- python bench.py --no-configs --no-cpu-baseline --lanes 1"
-                 "prof_default:500:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline");;
+    prof) args+=("prof_config2:400:GPU_MAX_HW_QUEUES=8 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof2 -o prof -- python bench.py --no-configs --no-cpu-baseline --lanes 1"
+                 "prof_default:500:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline --hw-queues 0");;
     bench) args+=("bench_full:500:python bench.py");;
   esac
 done
