@@ -41,10 +41,11 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=4)
-    p.add_argument("--batch", type=int, default=256,
+    p.add_argument("--batch", type=int, default=512,
                    help="images per GPU per step (one lane: 6.7k images/s at 16, 7.0k at 32-48, 7.1k at 64, "
-                        "7.0-7.3k at 128, 7.4k at 256 on one box (round 3): the per-call fixed costs -- K1's "
-                        "prologue and tail, the host head and tail of a call -- amortised; 9.2 GB of pixels)")
+                        "7.0-7.3k at 128, 7.4k at 256 on one box (round 3); two lanes, 8 queues: 8.70-8.72k at 256, "
+                        "8.80k at 512 (round 4): the per-call fixed costs -- K1's prologue and tail, the host head "
+                        "and tail of a call -- amortised; 18.4 GB of pixels)")
     p.add_argument("--lanes", type=int, default=2,
                    help="library lanes for every config of the run (phd_set_lanes; 2 is the library's default: "
                         "each call split into two concurrent halves, +10-13 %% images/s over 1).  With 2 the "
