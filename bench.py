@@ -276,7 +276,7 @@ def algorithmic_bytes(kernel, h, w):
     an implementation table, not counted)."""
     n, hwf = h * w, h * (w // 2 + 1)
     return {"hsv_stats": 3 * n, "palette_sums": 3 * n, "fft_rows": 3 * n + 16 * hwf,
-            "fft_cols": 16 * hwf, "report": 9 * n + 32 * hwf}.get(kernel)
+            "fft_cols": 16 * hwf, "blur_path": 3 * n + 32 * hwf, "report": 9 * n + 32 * hwf}[kernel]
 
 
 def per_kernel_roofline(warm, B, H, W):
@@ -676,7 +676,7 @@ def config3(cx, n=512, h=1080, w=1920, iters=10):
     lib.phd_profile_read(0, ctypes.byref(tot), ctypes.byref(cnt))
     lib.phd_profile_kernels(0)
     us = 1000 * tot.value / max(cnt.value, 1)
-    ab = 3.0 * n * h * w
+    ab = float(n * algorithmic_bytes("hsv_stats", h, w))
     del t
     torch.cuda.empty_cache()
     return {"workload": f"{n} x {h}x{w} RGB8, rgb2hsv + rgb_statistics only, device-resident",
@@ -691,9 +691,9 @@ def config4(cx, total, h=3000, w=4000, iters=3):
     """BASELINE config 4: `total` 4000x3000 images, FFT + blur-profile path alone
     (phd_blur_batch_device), sharded over the ranks with shard.assign (each rank
     one call over its device-resident share).  The column pass is this path's
-    dominant kernel: its algorithmic bytes are the half spectrum read plus the
-    bin map, 18 * H * (W/2+1) per image (SURVEY.md 8d counts 3N + 32 H Wf =
-    228 MB for the whole path, the `alg_bytes` counter)."""
+    dominant kernel: its algorithmic bytes are the half spectrum it reads,
+    16 * H * (W/2+1) per image (SURVEY.md 8d row 4, algorithmic_bytes("fft_cols");
+    the whole path is 3N + 32 H Wf = 228 MB, the `alg_bytes` counter)."""
     import numpy as np
     lib, torch = cx.lib, cx.torch
     from photohive_dsp_amd import shard
@@ -735,9 +735,8 @@ def config4(cx, total, h=3000, w=4000, iters=3):
     lib.phd_profile_kernels(0)
     del t
     torch.cuda.empty_cache()
-    wf = w // 2 + 1
-    m = cx.merge(elapsed, n, n * h * w, n * (3 * h * w + 32 * h * wf), us["fft_cols"] * n / 1000.0, n)
-    ab = 18.0 * h * wf
+    m = cx.merge(elapsed, n, n * h * w, n * algorithmic_bytes("blur_path", h, w), us["fft_cols"] * n / 1000.0, n)
+    ab = float(algorithmic_bytes("fft_cols", h, w))
     return {"workload": f"{total} x {h}x{w} RGB8 over {cx.world} GPU, FFT + blur_profile only, device-resident",
             "scaling": "strong", "n_gpus": cx.world, "images_per_gpu_max": int(np.ceil(total / cx.world)),
             "images_per_s": round(m["images"] / m["elapsed"], 1),
@@ -815,7 +814,7 @@ def plan_only(args, world, rank):
     c5 = shard.assign(sizes5, world)[rank]
     out = {}
     for name, n, pix, ab in (("config2", B, B * H * W, B * algorithmic_bytes("report", H, W)),
-                             ("config4", len(c4), len(c4) * H * W, len(c4) * (3 * H * W + 32 * H * (W // 2 + 1))),
+                             ("config4", len(c4), len(c4) * H * W, len(c4) * algorithmic_bytes("blur_path", H, W)),
                              ("config5", len(c5), sum(sizes5[i][0] * sizes5[i][1] for i in c5),
                               sum(algorithmic_bytes("report", *sizes5[i]) for i in c5))):
         m = shard.merge_counters([1.0 + rank, n, pix, ab])
@@ -826,6 +825,16 @@ def plan_only(args, world, rank):
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def dump_maps(tag):
+    """PHD_BENCH_MAPS=prefix: copy /proc/self/maps to prefix.<tag>.<pid> (crash
+    triage: a native backtrace's raw addresses resolve against these mappings
+    to library + offset, then addr2line / objdump on the same image)."""
+    pre = os.environ.get("PHD_BENCH_MAPS")
+    if pre:
+        with open("/proc/self/maps") as f, open(f"{pre}.{tag}.{os.getpid()}", "w") as g:
+            g.write(f.read())
 
 
 def main(argv=None):
@@ -863,9 +872,11 @@ def main(argv=None):
             dist.init_process_group(backend)
     import photohive_dsp_amd  # noqa: F401
     cx = Ctx(args, world, rank, backend)
+    dump_maps("ctx")
 
     cx.lib.phd_set_lanes(args.lanes)                  # every config of this run
     hl = headline(cx)
+    dump_maps("headline")
     extra = {}
     if hl["lanes"] > 1 and not args.no_one_lane:
         # the same workload on one lane: each launch alone on the GPU, so the

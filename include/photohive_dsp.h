@@ -238,6 +238,11 @@ int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int height, int widt
 int phd_debug_power_spectrum(const uint8_t* d_rgb, int height, int width, double* d_out);
 /* log_mant, the polar bins' table-driven fp64 log, over n positive device doubles. */
 int phd_debug_log_mant(const double* d_x, double* d_y, long n);
+/* Host only (no device needed): entries (runs of one polar bin + a sentinel)
+ * of the longest spectrum column of this size and bin grid.  Above 256 the
+ * compile-time column pass cannot hold the column's list and the size takes
+ * the runtime-plan FFT.  Returns the count or -1. */
+int phd_debug_col_runs_max(int height, int width, int radius_partitions, int angle_partitions);
 
 /* Validation hook for the global-memory FFTs behind sides above 8192 px and
  * lengths with a large prime factor (the reference's FFTW r2c takes any

@@ -267,12 +267,14 @@ hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftP
 template <int T, int MODE>
 static hipError_t cols_impl(const double2* inter, size_t inter_stride, int n, int height, int wf, int C,
                             const FftPlan& plan, const uint16_t* binmap, int nbins, int lds_bins, size_t lds,
-                            unsigned long long* bin_sums, double* fmax_part, long out_stride, hipStream_t st) {
+                            unsigned long long* bin_sums, double* fmax_part, long out_stride, double bscale,
+                            hipStream_t st) {
     static bool once = (allow_big_lds(k_fft_cols<T, MODE>), true);
     (void)once;
     static const int ablate = phd_knob("PHD_ABLATE") ? atoi(phd_knob("PHD_ABLATE")) : 0;   // debug only
     phd_launch((k_fft_cols<T, MODE>), dim3((wf + C - 1) / C, n), dim3(T), lds, st, inter, inter_stride, height,
-                       wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_part, out_stride, bin_scale(height, wf),
+                       wf, C, plan, binmap, nbins, lds_bins, bin_sums, fmax_part, out_stride,
+                       bscale > 0.0 ? bscale : bin_scale(height, wf),
                        ablate);
     return hipGetLastError();
 }
@@ -296,13 +298,13 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
 
 static hipError_t cols_t(const double2* inter0, size_t inter_stride, int n, int height, int wf, const FftPlan& plan,
                          const uint16_t* binmap, int nbins, unsigned long long* bin_sums0, double* fmax_part0, long out_stride,
-                         hipStream_t st) {
+                         hipStream_t st, double bscale = 0.0) {
     size_t lds;
     int lds_bins;
     const int C = fft_cols_blocks(height, wf, nbins, plan, &lds, &lds_bins);
     const size_t e = (size_t)C * height;
 #define PHD_COLS(T, M) cols_impl<T, M>(inter0, inter_stride, n, height, wf, C, plan, binmap, nbins, lds_bins, lds, \
-                                       bin_sums0, fmax_part0, out_stride, st)
+                                       bin_sums0, fmax_part0, out_stride, bscale, st)
     switch (plan_mode(plan)) {
         case 1: return e <= 2048 ? PHD_COLS(256, 1) : PHD_COLS(512, 1);
         case 3: return e <= 2048 ? PHD_COLS(256, 3) : PHD_COLS(512, 3);
@@ -320,8 +322,8 @@ hipError_t launch_fft_cols_batch(const double2* inter0, size_t inter_stride, int
 
 hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
                            const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
-                           double* fmax_part, hipStream_t st) {
-    return launch_fft_cols_batch(inter, 0, 1, height, wf, plan, binmap, nbins, bin_sums, fmax_part, 0, st);
+                           double* fmax_part, hipStream_t st, double bscale) {
+    return cols_t(inter, 0, 1, height, wf, plan, binmap, nbins, bin_sums, fmax_part, 0, st, bscale);
 }
 
 }  // namespace phd

@@ -353,15 +353,16 @@ hipError_t launch_split_t(const double2* Z, int height, int width, double2* inte
 }
 
 hipError_t launch_power_bins(const double2* X, int height, int wf, const uint16_t* binmap, int nbins,
-                             unsigned long long* bin_sums, double* fmax_part, hipStream_t st) {
+                             unsigned long long* bin_sums, double* fmax_part, hipStream_t st, double bscale) {
     const long total = (long)height * wf;
+    if (bscale <= 0.0) bscale = bin_scale(height, wf);
     const size_t lds = sizeof(unsigned long long) * nbins;
     if (lds <= 48 * 1024) {
         phd_launch(k_power_bins<true>, dim3(kPowerBinBlocks), dim3(256), lds, st, X, total, binmap, nbins, bin_sums,
-                   fmax_part, bin_scale(height, wf));
+                   fmax_part, bscale);
     } else {
         phd_launch(k_power_bins<false>, dim3(kPowerBinBlocks), dim3(256), 0, st, X, total, binmap, nbins, bin_sums,
-                   fmax_part, bin_scale(height, wf));
+                   fmax_part, bscale);
     }
     return hipGetLastError();
 }

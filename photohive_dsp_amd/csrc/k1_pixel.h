@@ -109,11 +109,15 @@ K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
     }
 }
 
-// c = floor(n2 / (Lh kd1)) for n2 = 120 X < 2^18: (n2 + 1/2) / (Lh kd1) lies
-// at least 1/2 / (Lh kd1) from an integer, and the fp32 form below (1 / Lh
-// times 1 / kd1, each correctly rounded, two products: ~2 ulp) errs by at most
-// (720 / Lh + 1) * 2.4e-7, eight times inside that margin for every Lh <= 360
-// and kd <= 255.
+// c = floor(n2 / (Lh kd1)) for n2 = 120 X < 2^18: q = (n2 + 1/2) / (Lh kd1)
+// lies at least 1/2 / (Lh kd1) from an integer, i.e. a relative margin of
+// 0.5 / (n2 + 0.5) >= 2.7e-6 (n2 < 120 * 6 * 255).  The fp32 form below
+// (n2 + 1/2 exact; 1 / Lh correctly rounded, 0.5 ulp; 1 / kd1 from
+// v_rcp_f32 on the device, <= 1 ulp, correctly rounded on the host; two
+// products, 0.5 ulp each) errs by at most 2.5 ulp = 3.0e-7 relative, nine
+// times inside the margin, so device and host agree on c for every Lh <= 360
+// and kd <= 255.  (tests/test_k1_pixel.py runs the host twin over the RGB
+// cube; test_table_k1_exhaustive_rgb_cube_palette runs the device kernel.)
 K1_HD int k1_halfbin(int n2, float rkd, const K1Grid& G) {
     return (int)(((float)n2 + 0.5f) * G.rlh * rkd);
 }

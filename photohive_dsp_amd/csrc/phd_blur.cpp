@@ -37,7 +37,7 @@ int newton_int_sqrt(double val) {       // src/utilities.c:43-52
 // T <= 1024 threads: at most 2046 bytes of run plus a 16-byte load
 constexpr size_t kBinMapPad = 4096;
 
-bool build_blur_table(int height, int width, int nr, int na, BlurTable* t) {
+bool build_blur_table(int height, int width, int nr, int na, BlurTable* t, bool upload) {
     const int wf = width / 2 + 1;
     t->height = height;
     t->wf = wf;
@@ -98,6 +98,10 @@ bool build_blur_table(int height, int width, int nr, int na, BlurTable* t) {
     t->counts.assign((size_t)na * nr, 0);
     for (unsigned i = 0; i < nth; i++)
         for (size_t b = 0; b < t->counts.size(); b++) t->counts[b] += part[i][b];
+    if (!upload) {
+        t->map = std::move(map);
+        return true;
+    }
     // + kBinMapPad bytes: the runtime-plan column kernels may load a run of bin
     // ids past the last column's end
     if (hipMalloc(&t->d_map, map.size() * sizeof(uint16_t) + kBinMapPad) != hipSuccess) {
@@ -123,7 +127,11 @@ bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r) 
         nrun[x] = n;
         stride = std::max(stride, n + 1);                  // + the sentinel
     }
-    if (stride > kColRunsMax || H > 65535) return false;
+    r->max_entries = stride;
+    if (stride > kColRunsMax || H > 65535) {
+        r->too_many = true;                                // a fixed property of the size: cached
+        return false;
+    }
     std::vector<uint32_t> runs((size_t)wf * stride, (uint32_t)H << 16);
     std::vector<uint8_t> seg((size_t)wf * T, 0);
     for (int x = 0; x < wf; x++) {
@@ -142,6 +150,10 @@ bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r) 
         hipMemcpy(r->d_runs, runs.data(), runs.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(r->d_seg, seg.data(), seg.size(), hipMemcpyHostToDevice) != hipSuccess) {
         set_error("upload of the column bin runs failed");
+        if (r->d_runs) (void)hipFree(r->d_runs);
+        if (r->d_seg) (void)hipFree(r->d_seg);
+        r->d_runs = nullptr;
+        r->d_seg = nullptr;
         return false;
     }
     r->T = T;
@@ -240,4 +252,19 @@ extern "C" void phd_free_pgm(Image_PGM* img) {
     if (!img) return;
     free(img->data);
     free(img);
+}
+
+extern "C" int phd_debug_col_runs_max(int height, int width, int radius_partitions, int angle_partitions) {
+    phd::BlurTable t;
+    if (height < 2 || width < 2 || radius_partitions < 1 || angle_partitions < 1 ||
+        !phd::build_blur_table(height, width, radius_partitions, angle_partitions, &t, false))
+        return -1;
+    int mx = 0;
+    for (int x = 0; x < t.wf; x++) {
+        const uint16_t* col = t.map.data() + (size_t)x * t.height;
+        int n = 1;
+        for (int u = 1; u < t.height; u++) n += col[u] != col[u - 1];
+        mx = std::max(mx, n + 1);
+    }
+    return mx;
 }

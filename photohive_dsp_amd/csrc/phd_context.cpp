@@ -83,15 +83,7 @@ Context* get_context_lane(int lane) {
         hipEventCreateWithFlags(&c->ev_k1, of) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_tail, of) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_dl_sd, of) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->fft, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_ws, of) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fft, of) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->fft2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->dl, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_rows[0], of) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_rows[1], of) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_cols[0], of) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_cols[1], of) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_null, of) != hipSuccess) {
         set_error("hipStreamCreate failed");
         delete c;
@@ -161,9 +153,21 @@ int lanes_setting() {
     return l;
 }
 
+namespace {
+// lanes the calling thread's current call really runs on (on_lanes sets it
+// around each lane's body; 1 outside a split call)
+thread_local int t_call_lanes = 1;
+}
+
+CallLanes::CallLanes(int n) : prev_(t_call_lanes) { t_call_lanes = n; }
+CallLanes::~CallLanes() { t_call_lanes = prev_; }
+
 int k1_blocks_per_cu() {
     static const int env = phd_knob("PHD_K1_BPC") ? std::max(1, std::min(2, atoi(phd_knob("PHD_K1_BPC")))) : 0;
-    return env ? env : (lanes_setting() >= 2 ? 1 : 2);
+    // one block per CU only when this call is split over two lanes: the other
+    // half of each CU then runs the other lane's FFT blocks; an unsplit call
+    // (small batch, caller stream, host APIs) keeps both blocks
+    return env ? env : (t_call_lanes >= 2 ? 1 : 2);
 }
 
 LaneWorker* lane_worker() {
@@ -343,9 +347,12 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
             auto f = c->colruns.find(key);
             if (f == c->colruns.end()) {
                 ColRuns r;
-                if (build_col_runs(tbl->map.data(), tbl->height, tbl->wf, T, &r)) f = c->colruns.emplace(key, r).first;
+                // a size whose columns hold too many runs is remembered as such
+                // (no rescan of the map per call); an upload error is not
+                if (build_col_runs(tbl->map.data(), tbl->height, tbl->wf, T, &r) || r.too_many)
+                    f = c->colruns.emplace(key, r).first;
             }
-            if (f != c->colruns.end()) runs = &f->second;
+            if (f != c->colruns.end() && f->second.d_runs) runs = &f->second;
             else ct = false;
         }
     }

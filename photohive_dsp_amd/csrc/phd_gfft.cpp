@@ -183,10 +183,11 @@ hipError_t generic_rows(const FftSel& s, const uint8_t* img, const double* pgm, 
 }
 
 hipError_t generic_cols(const FftSel& s, double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
-                        unsigned long long* bin_sums, double* fmax_part, hipStream_t st) {
-    if (s.cols_fused) return launch_fft_cols(inter, height, wf, s.pcol->plan, binmap, nbins, bin_sums, fmax_part, st);
+                        unsigned long long* bin_sums, double* fmax_part, hipStream_t st, double bscale) {
+    if (s.cols_fused)
+        return launch_fft_cols(inter, height, wf, s.pcol->plan, binmap, nbins, bin_sums, fmax_part, st, bscale);
     if (!gfft_run(*s.gcol, inter, inter, wf, s.gbuf, st)) return hipErrorLaunchFailure;
-    return launch_power_bins(inter, height, wf, binmap, nbins, bin_sums, fmax_part, st);
+    return launch_power_bins(inter, height, wf, binmap, nbins, bin_sums, fmax_part, st, bscale);
 }
 
 }  // namespace phd

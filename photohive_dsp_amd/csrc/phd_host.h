@@ -82,13 +82,16 @@ struct ColRuns {
     int T = 0, stride = 0;               // threads per column; entries per column (runs + sentinel)
     uint32_t* d_runs = nullptr;          // device [wf][stride]
     uint8_t* d_seg = nullptr;            // device [wf][T]
+    int max_entries = 0;                 // the longest column's runs + sentinel
+    bool too_many = false;               // max_entries > kColRunsMax: runtime-plan FFT for this size
 };
-// false when a column needs more than kColRunsMax entries (that size then
-// takes the runtime-plan FFT) or on an upload error.
+// false when a column needs more than kColRunsMax entries (too_many: that size
+// then takes the runtime-plan FFT) or on an upload error (nothing allocated).
 bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r);
 // Exact (phi_bin, r_bin) of every spectrum element, glibc atan2 + newton_int_sqrt
 // exactly as src/blur_profile.c:87-97 / 427-458.
-bool build_blur_table(int height, int width, int nr, int na, BlurTable* t);
+// upload == false: host map and counts only (no device copy)
+bool build_blur_table(int height, int width, int nr, int na, BlurTable* t, bool upload = true);
 void vectorize_blur(const double* bins, int na, int nr, double streak, double mag, int denom,
                     Blur_Vector* out10);
 
@@ -198,23 +201,14 @@ struct Context {
     size_t ptrs_bytes = 0;
     size_t stage_bytes = 0;
     hipEvent_t ev[8] = {};
-    // the palette's second pass (rules upload, Kcut, sums) runs on its own
-    // stream, concurrent with the FFTs: joined by events
+    // two streams per context: `stream` (K1, then the FFT chain) and `tail`
+    // (the A-record download, the palette's second pass -- rules upload, Kcut,
+    // partial sums -- concurrent with the FFTs, then each image's C-record
+    // download as soon as its column pass is done), joined by events
     hipStream_t tail = nullptr;
     hipEvent_t ev_k1 = nullptr, ev_tail = nullptr;
-    hipEvent_t ev_dl_sd = nullptr;                  // the download stream's last copy of a call
-    // the FFTs run on their own stream too: the compile-time row pass does not
-    // need K1, so it overlaps it (only the column pass waits for the sums)
-    hipStream_t fft = nullptr;
-    hipEvent_t ev_ws = nullptr, ev_fft = nullptr;
-    // two-stream FFT pipeline: row passes on `fft`, column passes on `fft2`,
-    // ping-pong intermediates, so image i+1's rows overlap image i's columns
-    hipStream_t fft2 = nullptr;
-    hipEvent_t ev_rows[2] = {}, ev_cols[2] = {};
-    // per-image download: image i's C record leaves on `dl` as soon as its
-    // column pass (ev_img_fft[i]) and the palette tail are done, so the host
-    // assembles image i while the FFTs of the later images run
-    hipStream_t dl = nullptr;
+    hipEvent_t ev_dl_sd = nullptr;                  // the tail stream's last copy of a call
+    hipEvent_t ev_fft = nullptr;                    // the FFT chain's end
     std::vector<hipEvent_t> ev_img_fft, ev_img_dl;
     KernelProfiler prof;
     hipEvent_t ev_null = nullptr;                   // orders the library stream after the null stream
@@ -316,8 +310,9 @@ bool select_generic(Context* c, int height, int width, int nbins, FftSel* s);
 hipError_t generic_rows(const FftSel& s, const uint8_t* img, const double* pgm, int height, int width,
                         const unsigned long long* sums, const double* avgd, const double* k255, double2* inter,
                         hipStream_t st);
+// (bscale: the bins' fixed-point scale, 0 = bin_scale(height, wf))
 hipError_t generic_cols(const FftSel& s, double2* inter, int height, int wf, const uint16_t* binmap, int nbins,
-                        unsigned long long* bin_sums, double* fmax_part, hipStream_t st);
+                        unsigned long long* bin_sums, double* fmax_part, hipStream_t st, double bscale = 0.0);
 const BlurTable* get_table(Context* c, int height, int width, int nr, int na);
 // Classification tables of a grid (uploaded once per configuration).
 const Context::Cls* get_cls(Context* c, const GridParams& gp);
@@ -330,11 +325,12 @@ bool check_crops(const Crop_Boundaries* cb, int height, int width);
 long hsv_count(int height, int width, int ds);
 // The Full_Report_Data tree (compile_full_report, src/utilities.c:210-226) from
 // the statistics, the palette decision and its slot sums pal[4k + {h, s, v, n}],
-// the polar bin sums (bin_scale fixed point) and spectrum max, the crop sums.
+// the polar bin sums (fixed point at bscale, 0 = bin_scale(H, Wf)) and
+// spectrum max, the crop sums.
 Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const PaletteDecision& dec,
                            const double* pal, long n_hsv, const BlurTable& tbl, const unsigned long long* bin_sums,
                            double fmax, const phd_config& cfg, const Crop_Boundaries* crops,
-                           const double* sharp_sums, std::string* why);
+                           const double* sharp_sums, std::string* why, double bscale = 0.0);
 // get_full_report_data on the caller's planar doubles (phd_planar.cpp): the
 // RGB8 pipeline when every value is k/255.0, else the fp64 planar kernels.
 Full_Report_Data* report_planar(Context* c, const double* r, const double* g, const double* b, int height,

@@ -52,12 +52,14 @@ constexpr int kMaxDirectPrime = 61;
 // strict threshold comparisons vectorize_blur_profile makes on them -- are the
 // same on every run whatever order the atomics land in.  The scale is the
 // largest power of two that keeps any bin of an H x Wf half spectrum below
-// 2^62: |X| <= N = H * W (pgm values lie in [0, 1]), so log p <= 2 ln N and a
-// bin holds at most H * Wf elements (2^-35 per element at 4000x3000, 2^-41
-// at 640x480; 2^-30 at the reference's 120 MP limit).
-inline double bin_scale(int height, int wf) {
+// 2^62: |X| <= N * M with M >= |pgm - avg| (M = 1 for RGB8 images, whose luma
+// lies in [0, 1]; the planar path passes its luma range), so log p <= 2 ln(N M)
+// and a bin holds at most H * Wf elements (2^-35 per element at 4000x3000,
+// 2^-41 at 640x480; 2^-30 at the reference's 120 MP limit).
+inline double bin_scale(int height, int wf, double lrange = 1.0) {
     const double n = (double)height * (2.0 * wf);
-    const double bound = (double)height * wf * 2.0 * __builtin_log(n > 2.0 ? n : 2.0) + 1.0;
+    const double m = lrange > 1.0 ? lrange : 1.0;
+    const double bound = (double)height * wf * 2.0 * (__builtin_log(n > 2.0 ? n : 2.0) + __builtin_log(m)) + 1.0;
     return __builtin_ldexp(1.0, 62 - (int)__builtin_ceil(__builtin_log2(bound)));
 }
 
@@ -157,11 +159,19 @@ struct FftPlan {
 extern int g_ablate;   // ablation mask read by kernels under phd_debug_time_kernel
 int env_ablate();      // PHD_ABLATE (timing builds only)
 int num_cus();         // compute units of the current device
-// K1's two-block form: blocks per CU (2; 1 when device batches run on two
+// K1's two-block form: blocks per CU (2; 1 when this call runs split over two
 // lanes, so a K1 launch leaves half of every CU to the other lane's FFT
 // blocks: 7.89k against 7.66k images/s with two lanes, and 6.78k against
 // 7.07k with one, where K1 runs alone; PHD_K1_BPC overrides)
 int k1_blocks_per_cu();
+// Scope guard: the calling thread's current call runs on n lanes (on_lanes)
+struct CallLanes {
+    explicit CallLanes(int n);
+    ~CallLanes();
+    CallLanes(const CallLanes&) = delete;
+    CallLanes& operator=(const CallLanes&) = delete;
+    int prev_;
+};
 // hsv/stats/histogram pass over one image (K1).  ds = downsample rate.
 // K1 over a batch of same-size images (ds == 1); d_imgs is a device array of
 // n image pointers; image i's records sit at out0 + i * a_stride (sums, hist,
@@ -251,9 +261,10 @@ hipError_t launch_fft_rows(const uint8_t* img, int height, int width, const FftP
 // Column pass + epilogue: power, running max, sum log(p) over p >= 1 per
 // polar bin (binmap[wf][height], uint16 bin ids).  Accumulates into
 // bin_sums[na*nr] (bin_scale fixed point) and writes one max power per block to fmax_part.
+// (bscale: the fixed-point scale, 0 = bin_scale(height, wf))
 hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPlan& plan,
                            const uint16_t* binmap, int nbins, unsigned long long* bin_sums,
-                           double* fmax_part, hipStream_t st);
+                           double* fmax_part, hipStream_t st, double bscale = 0.0);
 // Column blocks of launch_fft_cols (= entries of fmax_part); optional LDS size.
 int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds, int* lds_bins);
 
@@ -409,9 +420,10 @@ constexpr int kPlanarBlocks = 1024;
 // flags: bit 0 not an 8-bit image, bit 1 non-finite value, bit 2 group index out of range
 hipError_t launch_planar_to_u8(const PlanarSrc& P, long n, uint8_t* rgb, int* flags, hipStream_t st);
 int planar_blocks(long n);   // partials of launch_planar_stats (per channel)
-// part1 / part2 [planar_blocks][3]: sums of x and of (x - mean)^2; *avg = (Br + Bg + Bb) / 3; pgm = luma plane
+// part1 / part2 [planar_blocks][3]: sums of x and of (x - mean)^2; *avg = (Br + Bg + Bb) / 3; pgm = luma plane;
+// lrng [planar_blocks][2]: -min and max of the luma per block
 hipError_t launch_planar_stats(const PlanarSrc& P, long n, double* pgm, double* part1, double* part2, double* avg,
-                               int* flags, hipStream_t st);
+                               double* lrng, int* flags, hipStream_t st);
 hipError_t launch_planar_k1(const PlanarSrc& P, int height, int width, int ds, const GridParams& gp, unsigned* hist,
                             unsigned short* chunk_hist, double* s_part, int* flags, hipStream_t st);
 hipError_t launch_planar_tail(const PlanarSrc& P, int height, int width, int ds, const GridParams& gp,
@@ -440,7 +452,7 @@ hipError_t launch_pairs(const uint8_t* img, const double* pgm, int height, int w
 hipError_t launch_split_t(const double2* Z, int height, int width, double2* inter, hipStream_t st);
 // Power, max partials (kPowerBinBlocks) and polar log-binning of inter [wf][H].
 hipError_t launch_power_bins(const double2* X, int height, int wf, const uint16_t* binmap, int nbins,
-                             unsigned long long* bin_sums, double* fmax_part, hipStream_t st);
+                             unsigned long long* bin_sums, double* fmax_part, hipStream_t st, double bscale = 0.0);
 
 hipError_t launch_debug_hsv(const uint8_t* img, long n, const GridParams& gp, const FastCls& fc,
                             const ClassTables* tabs, const double* k255, int* gid, double* hsv, hipStream_t st);

@@ -10,7 +10,9 @@
 // path (fft_global.hip) on the fp64 luma plane.  Values the reference cannot
 // handle (non-finite, or a group index past the octree: values above 1 can
 // index out of bounds in arm_octree, src/color_quantization.c:131-145) are
-// rejected with NULL, like its other undefined cases.
+// rejected with NULL, like its other undefined cases.  Any other finite values
+// (negative channels, luma outside [0, 1]) get a report: the polar bins'
+// fixed-point scale follows the image's largest |pgm - avg| (bin_scale).
 #include <cmath>
 #include <cstring>
 
@@ -25,7 +27,7 @@ size_t al(size_t x) { return (x + kAl - 1) / kAl * kAl; }
 
 // device / pinned-free host records of one planar call
 struct PRec {
-    size_t flags, avg, part1, part2, hist, spart, chunk, rules, search, off, pal, bins, fmax, sharp, total;
+    size_t flags, avg, lrng, part1, part2, hist, spart, chunk, rules, search, off, pal, bins, fmax, sharp, total;
 };
 
 PRec prec_layout(int nb, int tl, int nchunks, int nbins, int ncolblocks, int ncrops) {
@@ -38,6 +40,7 @@ PRec prec_layout(int nb, int tl, int nchunks, int nbins, int ncolblocks, int ncr
     };
     R.flags = take(sizeof(int));
     R.avg = take(sizeof(double));
+    R.lrng = take(sizeof(double) * 2 * nb);
     R.part1 = take(sizeof(double) * 3 * nb);
     R.part2 = take(sizeof(double) * 3 * nb);
     R.hist = take(sizeof(unsigned) * tl);
@@ -123,7 +126,28 @@ Full_Report_Data* report_planar(Context* c, const double* r, const double* g, co
     PHD_HIPN(hipMemsetAsync(dr, 0, R.total, st));
     // ---- the fp64 planar pipeline -------------------------------------------------
     double* avg = (double*)(dr + R.avg);
-    PHD_HIPN(launch_planar_stats(P, n, pgm, (double*)(dr + R.part1), (double*)(dr + R.part2), avg, flags, st));
+    PHD_HIPN(launch_planar_stats(P, n, pgm, (double*)(dr + R.part1), (double*)(dr + R.part2), avg,
+                                 (double*)(dr + R.lrng), flags, st));
+    // |pgm - avg| <= max(max - avg, avg - min) bounds every spectrum element
+    // (|X| <= N max|pgm - avg|): the polar bins' fixed-point scale
+    std::vector<double> lr(2 * nb + 1);
+    PHD_HIPN(hipMemcpyAsync(lr.data(), dr + R.avg, sizeof(double), hipMemcpyDeviceToHost, st));
+    PHD_HIPN(hipMemcpyAsync(lr.data() + 1, dr + R.lrng, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, st));
+    PHD_HIPN(hipStreamSynchronize(st));
+    const double av = lr[0];
+    double lrange = 0.0;                                   // (NaN propagates: a non-finite channel)
+    for (int k = 0; k < nb; k++) {
+        const double nlo = lr[1 + 2 * k], hi = lr[2 + 2 * k];   // -min, max of block k
+        const double m = std::max(hi - av, av + nlo);
+        lrange = (m != m || lrange != lrange) ? NAN : std::max(lrange, m);
+    }
+    if (!(lrange < 1e100) || av != av) {
+        set_error(std::isfinite(lrange) && av == av ? "Error: channel values too large for a finite power spectrum."
+                                                    : "Error: channel values must be finite (NaN or infinity in the "
+                                                      "image).");
+        return nullptr;
+    }
+    const double bscale = bin_scale(height, wf, lrange);
     PHD_HIPN(launch_planar_k1(P, height, width, ds, gp, (unsigned*)(dr + R.hist), (unsigned short*)(dr + R.chunk),
                               (double*)(dr + R.spart), flags, st));
     std::vector<uint8_t> h(R.total);
@@ -134,7 +158,7 @@ Full_Report_Data* report_planar(Context* c, const double* r, const double* g, co
     unsigned long long* bins = (unsigned long long*)(dr + R.bins);
     double* fmx = (double*)(dr + R.fmax);
     PHD_HIPN(generic_rows(fs, nullptr, pgm, height, width, nullptr, avg, c->d_k255, c->d_inter, st));
-    PHD_HIPN(generic_cols(fs, c->d_inter, height, wf, tbl->d_map, nbins, bins, fmx, st));
+    PHD_HIPN(generic_cols(fs, c->d_inter, height, wf, tbl->d_map, nbins, bins, fmx, st, bscale));
     if (ncrops) {
         // get_variance_sharpness runs on the luma before the DC removal (src/interface.c:70-73)
         std::vector<int> ca(4 * ncrops);
@@ -150,13 +174,11 @@ Full_Report_Data* report_planar(Context* c, const double* r, const double* g, co
     }
     PHD_HIPN(hipEventSynchronize(c->ev[5]));
     const int hf = *(const int*)(h.data() + R.flags);
-    if (hf & (2 | 4 | 8)) {
+    if (hf & (2 | 4)) {
         (void)hipStreamSynchronize(st);
         set_error(hf & 2 ? "Error: channel values must be finite (NaN or infinity in the image)."
-                  : hf & 4 ? "Error: channel values above 1 put pixels outside the octree (out-of-bounds group in "
-                             "arm_octree)."
-                           : "Error: luma values outside [0, 1] (a pixel downsample_rgb does not sample); this "
-                             "library's polar-bin sums require channel values in [0, 1].");
+                         : "Error: channel values put pixels outside the octree (out-of-bounds group in "
+                           "arm_octree).");
         return nullptr;
     }
     // get_rgb_statistics: the partials in the order the device summed them
@@ -198,7 +220,7 @@ Full_Report_Data* report_planar(Context* c, const double* r, const double* g, co
     for (int k = 0; k < fs.col_blocks; k++) fmax = fpart[k] > fmax ? fpart[k] : fmax;
     Full_Report_Data* out = assemble(stt, s_acc / (double)n_hsv, dec, (const double*)(h.data() + R.pal), n_hsv, *tbl,
                                      (const unsigned long long*)(h.data() + R.bins), fmax, cfg, crops,
-                                     (const double*)(h.data() + R.sharp), &why);
+                                     (const double*)(h.data() + R.sharp), &why, bscale);
     if (!out) set_error(why);
     return out;
 }

@@ -28,12 +28,6 @@
 
 namespace phd {
 
-// PHD_FFT_OVERLAP=1 (compile-time plans): see run_reports
-static bool overlap_env() {
-    static const bool v = phd_knob("PHD_FFT_OVERLAP") != nullptr;
-    return v;
-}
-
 namespace {
 
 constexpr size_t kAlign = 256;
@@ -145,10 +139,10 @@ float ms_between(hipEvent_t a, hipEvent_t b) {
 // sums of log(p); calculate_blur_profile's averaging (src/blur_profile.c:106-116);
 // vectorize_blur_profile (src/blur_profile.c:324-416).  flat: na x nr.
 void finish_blur(const BlurTable& tbl, const unsigned long long* bin_sums, double fmax, const phd_config& cfg,
-                 double* flat, Blur_Vector* vectors) {
+                 double* flat, Blur_Vector* vectors, double bscale = 0.0) {
     const int na = cfg.angle_partitions, nr = cfg.radius_partitions;
     const double gs = 1 / (2 * std::log(std::sqrt(fmax) + 1));
-    const double scale = bin_scale(tbl.height, tbl.wf);
+    const double scale = bscale > 0.0 ? bscale : bin_scale(tbl.height, tbl.wf);
     for (size_t b = 0; b < (size_t)na * nr; b++) {
         const double q = (double)tbl.counts[b];
         // the device sums are bin_scale fixed point (order-independent)
@@ -240,7 +234,7 @@ size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const PaletteDecision& dec,
                            const double* pal, long n_hsv, const BlurTable& tbl, const unsigned long long* bin_sums,
                            double fmax, const phd_config& cfg, const Crop_Boundaries* crops,
-                           const double* sharp_sums, std::string* why) {
+                           const double* sharp_sums, std::string* why, double bscale) {
     const int np = (int)dec.parents.size();
     const int na = cfg.angle_partitions, nr = cfg.radius_partitions;
     const int nsh = crops ? (crops->N > 0 ? crops->N : 1) : 0;
@@ -310,7 +304,7 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
     bv->len_vectors = 10;
     bv->blur_vectors = (Blur_Vector*)(blk + o_vec);
     memset(bv->blur_vectors, 0, sizeof(Blur_Vector) * 10);    // calloc in the reference
-    finish_blur(tbl, bin_sums, fmax, cfg, rows, bv->blur_vectors);
+    finish_blur(tbl, bin_sums, fmax, cfg, rows, bv->blur_vectors, bscale);
     Sharpnesses* sh = nullptr;
     if (crops) {   // get_variance_sharpness (src/filtering.c:151-183)
         sh = (Sharpnesses*)(blk + o_sh);
@@ -473,11 +467,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         c->ev_img_fft.push_back(a);
         c->ev_img_dl.push_back(b);
     }
-    // a failed earlier call may have left work on the side streams
+    // a failed earlier call may have left work on the side stream
     PHD_HIP(hipStreamSynchronize(c->tail));
-    PHD_HIP(hipStreamSynchronize(c->fft));
-    PHD_HIP(hipStreamSynchronize(c->fft2));
-    PHD_HIP(hipStreamSynchronize(c->dl));
     const GridParams gp = make_grid(cfg);
     const int ds = cfg.downsample_rate > 1 ? cfg.downsample_rate : 1;
     const long n_hsv = hsv_count(height, width, ds);
@@ -495,8 +486,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const size_t inter_one = sizeof(double2) * inter_elems(height, width);
     static const bool ctbatch_off = phd_knob("PHD_CT_NO_BATCH") != nullptr;
     const int q_ct = (int)std::min<size_t>((size_t)n, ((size_t)128 << 20) / inter_one);
-    const bool ct_batchable = !ctbatch_off && !overlap_env() && !phd_knob("PHD_FFT_PIPE") && n > 1 && q_ct >= 2 &&
-                              ((height + 1) / 2) % 4 == 0;
+    const bool ct_batchable = !ctbatch_off && n > 1 && q_ct >= 2 && ((height + 1) / 2) % 4 == 0;
     if (!select_fft(c, height, width, nbins, d_imgs, n, &fs, tbl, ct_batchable)) return false;
     const Context::Cls* cls = get_cls(c, gp);
     if (!cls) return false;
@@ -512,20 +502,14 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     auto dl_end = [&](int i) { return (i + 1) % dl_group == 0 || i == n - 1; };
     auto dl_last = [&](int i) { return std::min(n - 1, (i / dl_group + 1) * dl_group - 1); };
     // fused palette (one pixel pass): ds == 1 and the fused K1's LDS fits; else K1 + K3
-    static const bool two_pass = phd_knob("PHD_PALETTE_TWO_PASS") != nullptr;
-    const bool fused = ds <= 1 && !two_pass && fused_palette_ok(gp);
+    const bool fused = ds <= 1 && fused_palette_ok(gp);
     const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks, fused ? HueCells::count(gp) : 0);
     // half-spectrum intermediates: one per image of a group of Q (the group's row
-    // passes run before its column passes; measured best at Q = 1)
+    // passes run before its column passes); large images one at a time, so the
+    // intermediate stays in the 256 MB MALL between its two passes (round 2:
+    // a two-stream pipeline of rows i+1 beside columns i measured 10 % slower)
     // (+ 1024 elements of scratch past the tiles for the row pass's dummy stores)
-    static const int qcap = phd_knob("PHD_FFT_GROUP") ? atoi(phd_knob("PHD_FFT_GROUP")) : 0;
-    int Q = std::min(n, qcap > 0 ? qcap : 1);   // 1: the intermediate stays in the 256 MB MALL
-    while (Q > 1 && (size_t)Q * inter_one > ((size_t)2 << 30)) Q = (Q + 1) / 2;
-    // PHD_FFT_PIPE=1: a two-stream pipeline (rows of image i+1 beside the
-    // columns of image i, two intermediates).  Measured slower (5.2k vs 5.8k
-    // images/s at 4000x3000: the two 96 MB intermediates no longer share the
-    // MALL with the pixels), so the FFTs run serially on one stream by default.
-    static const bool pipe_env = phd_knob("PHD_FFT_PIPE") != nullptr;
+    int Q = 1;
     // runtime-plan sizes: the passes of a group of images are one launch each
     // (grid.y = image), the group's intermediates within 128 MB (half the
     // MALL); small images are otherwise bound by per-launch latency
@@ -534,9 +518,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (gbatch) Q = std::max(1, std::min(n, (int)(((size_t)128 << 20) / inter_one)));
     const bool ctbatch = fs.ct && ct_batchable && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
     if (ctbatch) Q = q_ct;
-    const bool pipe = !gbatch && !ctbatch && !fs.generic && Q == 1 && n > 1 && pipe_env;
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
-        !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)(pipe ? 2 : Q) * inter_one))
+        !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)Q * inter_one))
         return false;
     uint8_t* dw = (uint8_t*)c->d_ws;
     uint8_t* hp = (uint8_t*)c->h_pin;
@@ -552,7 +535,6 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     }
 
     PHD_HIP(hipMemsetAsync(dw, 0, (size_t)n * (L.a_bytes + L.c_bytes), st));
-    PHD_HIP(hipEventRecord(c->ev_ws, st));
     // An unprofiled one-launch K1 records its stage events with its own
     // dispatch and completion (no marker packets between it and the first row
     // pass), and ev[1] then stands for ev_k1; the A records go down on the
@@ -570,54 +552,16 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (!k1_rec) PHD_HIP(hipEventRecord(c->ev[1], st));
     const hipEvent_t ev_k1 = k1_rec ? c->ev[1] : c->ev_k1;
     if (!k1_rec) PHD_HIP(hipEventRecord(c->ev_k1, st));
-    const hipStream_t sa = k1_rec ? c->dl : st;
+    // the A records go down on the side stream (tail), beside the FFTs
+    const hipStream_t sa = k1_rec ? c->tail : st;
     if (sa != st) PHD_HIP(hipStreamWaitEvent(sa, ev_k1, 0));
     PHD_HIP(hipMemcpyAsync(hp, dw, (size_t)n * L.a_bytes, hipMemcpyDeviceToHost, sa));
     PHD_HIP(hipEventRecord(c->ev[5], sa));
-    // PHD_FFT_OVERLAP=1 (compile-time plans): the row pass sums the channels
-    // itself (the column pass's DC bias), so the FFT chain needs nothing from
-    // K1 and runs beside it on its own stream.  Measured slower (5.75k vs 6.05k
-    // images/s: row passes sharing CUs with K1 take 92 us instead of 49), so by
-    // default the FFTs follow K1 (and its records' download) on K1's stream and
-    // take its channel sums: a cross-stream event wait left the GPU idle
+    // The FFT chain follows K1 on its stream and takes its channel sums (the
+    // column pass's DC bias): a cross-stream event wait left the GPU idle
     // ~20 us between K1 and the first row pass.
-    const bool own_dc = fs.ct && overlap_env();
-    const hipStream_t sf = (pipe || own_dc) ? c->fft : st;
-    if (sf != st) {
-        PHD_HIP(hipStreamWaitEvent(sf, c->ev_ws, 0));
-        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sf, ev_k1, 0));
-    }
+    const hipStream_t sf = st;
     const size_t inter_elems = inter_one / sizeof(double2);
-    const hipStream_t sc = c->fft2;
-    if (pipe) {
-        if (!own_dc) PHD_HIP(hipStreamWaitEvent(sc, ev_k1, 0));   // DC removal needs K1's sums
-        PHD_HIP(hipStreamWaitEvent(sc, c->ev_ws, 0));
-        for (int i = 0; i < n; i++) {
-            const int b = i & 1;
-            double2* inter = c->d_inter + (size_t)b * inter_elems;
-            unsigned long long* rsum = own_dc ? (unsigned long long*)(dw + L.C(n, i) + L.c_rsum) : nullptr;
-            const unsigned long long* sums = own_dc ? rsum : (const unsigned long long*)(dw + L.A(i) + L.a_sums);
-            if (i >= 2) PHD_HIP(hipStreamWaitEvent(sf, c->ev_cols[b], 0));   // image i-2's columns are done
-            int ps = c->prof.begin(kFftRows, sf);
-            PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255, inter, sf, rsum));
-            c->prof.end(ps, sf);
-            PHD_HIP(hipEventRecord(c->ev_rows[b], sf));
-            PHD_HIP(hipStreamWaitEvent(sc, c->ev_rows[b], 0));
-            auto* bins = (unsigned long long*)(dw + L.C(n, i) + L.c_bins);
-            double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
-            ps = c->prof.begin(kFftCols, sc);
-            PHD_HIP(launch_cols_sel(fs, inter, height, width, wf, tbl->d_map, nbins, bins, fmx, sums, nullptr, sc));
-            c->prof.end(ps, sc);
-            if (ncrops) {
-                PHD_HIP(launch_sharpness(d_imgs[i], height, width, ncrops, crop_arr.data(),
-                                         crop_arr.data() + ncrops, crop_arr.data() + 2 * ncrops,
-                                         crop_arr.data() + 3 * ncrops, c->d_k255,
-                                         (double*)(dw + L.C(n, i) + L.c_sharp), sc));
-            }
-            PHD_HIP(hipEventRecord(c->ev_cols[b], sc));
-            if (dl_end(i)) PHD_HIP(hipEventRecord(c->ev_img_fft[i], sc));
-        }
-    }
     for (int g0 = 0; gbatch && g0 < n; g0 += Q) {
         const int g1 = std::min(n, g0 + Q);
         const uint8_t* const* d_ptrs = (const uint8_t* const*)(dw + L.P_dev(n));
@@ -664,20 +608,17 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             if (dl_end(i)) PHD_HIP(hipEventRecord(c->ev_img_fft[i], sf));
         }
     }
-    for (int g0 = 0; g0 < (pipe || gbatch || ctbatch ? 0 : n); g0 += Q) {
+    for (int g0 = 0; g0 < (gbatch || ctbatch ? 0 : n); g0 += Q) {
         const int g1 = std::min(n, g0 + Q);
         for (int i = g0; i < g1; i++) {
             const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
-            unsigned long long* rsum = own_dc ? (unsigned long long*)(dw + L.C(n, i) + L.c_rsum) : nullptr;
             const int ps = c->prof.begin(kFftRows, sf);
             PHD_HIP(launch_rows_sel(fs, d_imgs[i], height, width, sums, c->d_k255,
-                                    c->d_inter + (size_t)(i - g0) * inter_elems, sf, rsum));
+                                    c->d_inter + (size_t)(i - g0) * inter_elems, sf, nullptr));
             c->prof.end(ps, sf);
         }
-        if (g0 == 0 && fs.ct && !own_dc && sf != st) PHD_HIP(hipStreamWaitEvent(sf, ev_k1, 0));
         for (int i = g0; i < g1; i++) {
-            const unsigned long long* sums = own_dc ? (const unsigned long long*)(dw + L.C(n, i) + L.c_rsum)
-                                                    : (const unsigned long long*)(dw + L.A(i) + L.a_sums);
+            const unsigned long long* sums = (const unsigned long long*)(dw + L.A(i) + L.a_sums);
             auto* bins = (unsigned long long*)(dw + L.C(n, i) + L.c_bins);
             double* fmx = (double*)(dw + L.C(n, i) + L.c_fmax);
             const int ps = c->prof.begin(kFftCols, sf);
@@ -704,8 +645,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         }
     }
     // the last column pass ends the FFT work (it waited for the last row pass)
-    PHD_HIP(hipEventRecord(c->ev[2], pipe ? sc : sf));
-    PHD_HIP(hipEventRecord(c->ev_fft, pipe ? sc : sf));
+    PHD_HIP(hipEventRecord(c->ev[2], sf));
+    PHD_HIP(hipEventRecord(c->ev_fft, sf));
 
     // host decisions while the FFTs run
     const auto t_enq = std::chrono::steady_clock::now();
@@ -771,9 +712,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         max_slots = std::max(max_slots, h_ns[i]);
     }
     // the second pass on the tail stream, after K1, concurrent with the FFTs
-    static const bool tail_on_fft = phd_knob("PHD_TAIL_ON_FFT") != nullptr;
-    const hipStream_t s2 = tail_on_fft ? (pipe ? sc : sf) : c->tail;
-    PHD_HIP(hipStreamWaitEvent(s2, ev_k1, 0));
+    const hipStream_t s2 = c->tail;
+    if (sa != s2) PHD_HIP(hipStreamWaitEvent(s2, ev_k1, 0));
     uint8_t* hb = hp + (size_t)n * (L.a_bytes + L.c_bytes);
     const bool batched = ds <= 1 && (fused || palette_sums_b_lds(gp.tl, max_slots) <= 160 * 1024);
     // the B records (and, batched, the Kcut list right after them): one copy
@@ -833,23 +773,24 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // another stream costs ~30 us of idle GPU): a single image's palette tail
     // (decisions, Kcut, partial sums) ends after its FFTs, a batch's FFTs end
     // after the tail
-    const bool last_on_st = sf == st && !pipe;
-    const bool tail_last = last_on_st && n == 1;
+    const bool last_on_st = true;                             // the FFTs run on st
+    const bool tail_last = n == 1;
     if (!tail_last) {
         PHD_HIP(hipStreamWaitEvent(st, c->ev_tail, 0));
-        if (sf != st || pipe) PHD_HIP(hipStreamWaitEvent(st, c->ev_fft, 0));
         PHD_HIP(hipEventRecord(c->ev[3], st));
     } else {
         PHD_HIP(hipStreamWaitEvent(s2, c->ev_fft, 0));
         PHD_HIP(hipEventRecord(c->ev[3], s2));
     }
     // image i's C record (bins, max partials, palette sums, sharpness) goes to
-    // the host once its column pass and the palette tail are done; the host
-    // assembles it while the later images' FFTs run
+    // the host once its column pass and the palette tail are done (on the tail
+    // stream, after the tail's kernels); the host assembles it while the later
+    // images' FFTs run.  Two streams per lane: two lanes fit HIP's default
+    // four hardware queues (round 5: five streams per lane needed
+    // GPU_MAX_HW_QUEUES=8 to keep unrelated work from sharing a queue)
     uint8_t* hc = hp + (size_t)n * L.a_bytes;
-    const hipStream_t sd = c->dl;
-    const hipStream_t s_end = tail_last ? s2 : st;           // last_on_st: the last group's stream
-    PHD_HIP(hipStreamWaitEvent(sd, c->ev_tail, 0));
+    const hipStream_t sd = s2;
+    const hipStream_t s_end = tail_last ? s2 : st;           // the last group's stream
     bool sd_used = false;
     for (int i0 = 0; i0 < n; i0 = dl_last(i0) + 1) {
         const int i1 = dl_last(i0);
@@ -1151,6 +1092,7 @@ static void on_lanes(Context* c0, bool want, F&& body) {
     LaneWorker* lw = c1 ? lane_worker() : nullptr;
     if (!lw || !lw->try_acquire()) {
         std::lock_guard<std::mutex> lk(c0->mu);
+        CallLanes cl(1);
         body(c0, 0, 1);
         return;
     }
@@ -1162,12 +1104,14 @@ static void on_lanes(Context* c0, bool want, F&& body) {
         (void)hipSetDevice(dev);
         {
             std::lock_guard<std::mutex> lk1(c1->mu);
+            CallLanes cl(2);
             body(c1, 1, 2);
         }
         err1 = phd_last_error();
     });
     {
         std::lock_guard<std::mutex> lk(c0->mu);
+        CallLanes cl(2);
         body(c0, 0, 2);
     }
     lw->wait();

@@ -28,10 +28,11 @@ constexpr int kPT = 256;
 
 // flags (device int): bit 0 some value is not k/255 (not an 8-bit image);
 // bit 1 a value is not finite; bit 2 a pixel's group index falls outside the
-// octree (values above 1: the reference indexes out of bounds); bit 3 a luma
-// value outside [0, 1] (any pixel, sampled by downsample_rgb or not): the
-// polar bins' fixed point (bin_scale) assumes |pgm - avg| <= 1
-constexpr int kFlagNotU8 = 1, kFlagNonFinite = 2, kFlagGroupRange = 4, kFlagLumaRange = 8;
+// octree (values above 1: the reference indexes out of bounds).  Any other
+// finite values are the reference's to report on: negative channels, luma
+// outside [0, 1] (the polar bins' fixed-point scale follows the observed luma
+// range, bin_scale)
+constexpr int kFlagNotU8 = 1, kFlagNonFinite = 2, kFlagGroupRange = 4;
 
 __device__ __forceinline__ void flag_wave(int* flags, bool bad, int bit) {
     if (__any(bad) && lane_id() == 0) atomicOr(flags, bit);
@@ -68,15 +69,18 @@ __global__ __launch_bounds__(kPT) void k_planar_to_u8(PlanarSrc P, long n, uint8
     }
 }
 
-// Channel sums (one partial per block and channel: part[3 * block + c]) and
-// the luma plane pgm = 0.299 r + 0.587 g + 0.114 b.
+// Channel sums (one partial per block and channel: part[3 * block + c]), the
+// luma plane pgm = 0.299 r + 0.587 g + 0.114 b and its range per block
+// (lrng[2 * block] = -min, lrng[2 * block + 1] = max; -inf for no pixel).
 __global__ __launch_bounds__(kPT) void k_planar_moments(PlanarSrc P, long n, double* __restrict__ pgm,
-                                                        double* __restrict__ part, int* __restrict__ flags) {
+                                                        double* __restrict__ part, double* __restrict__ lrng,
+                                                        int* __restrict__ flags) {
     __shared__ double red[kPT / 64];
     double s[3] = {0.0, 0.0, 0.0};
+    double nlo = -__builtin_inf(), hi = -__builtin_inf();
     for (long i0 = (long)blockIdx.x * kPT; i0 < n; i0 += (long)gridDim.x * kPT) {
         const long i = i0 + threadIdx.x;
-        bool bad = false, out = false;
+        bool bad = false;
         if (i < n) {
             const double r = P.r[i], g = P.g[i], b = P.b[i];
             bad = !isfinite(r) || !isfinite(g) || !isfinite(b);
@@ -85,14 +89,23 @@ __global__ __launch_bounds__(kPT) void k_planar_moments(PlanarSrc P, long n, dou
             s[2] += b;
             const double y = 0.299 * r + 0.587 * g + 0.114 * b;
             pgm[i] = y;
-            out = !(y >= -1e-12 && y <= 1.0 + 1e-12);          // (0.299 + 0.587 + 0.114 rounds above 1)
+            nlo = fmax(nlo, -y);
+            hi = fmax(hi, y);
         }
         flag_wave(flags, bad, kFlagNonFinite);
-        flag_wave(flags, out, kFlagLumaRange);
     }
     for (int c = 0; c < 3; c++) {
         const double t = block_sum(s[c], red);
         if (threadIdx.x == 0) part[3 * blockIdx.x + c] = t;
+    }
+    double m[2] = {nlo, hi};
+    for (int k = 0; k < 2; k++) {
+        double x = wave_max(m[k]);
+        __syncthreads();
+        if (lane_id() == 0) red[threadIdx.x >> 6] = x;
+        __syncthreads();
+        for (int q = 0; q < kPT / 64; q++) x = fmax(x, red[q]);
+        if (threadIdx.x == 0) lrng[2 * blockIdx.x + k] = x;
     }
 }
 
@@ -337,9 +350,9 @@ hipError_t launch_planar_to_u8(const PlanarSrc& P, long n, uint8_t* rgb, int* fl
 int planar_blocks(long n) { return (int)grid_for(n); }
 
 hipError_t launch_planar_stats(const PlanarSrc& P, long n, double* pgm, double* part1, double* part2, double* avg,
-                               int* flags, hipStream_t st) {
+                               double* lrng, int* flags, hipStream_t st) {
     const unsigned nb = grid_for(n);
-    phd_launch(k_planar_moments, dim3(nb), dim3(kPT), 0, st, P, n, pgm, part1, flags);
+    phd_launch(k_planar_moments, dim3(nb), dim3(kPT), 0, st, P, n, pgm, part1, lrng, flags);
     phd_launch(k_planar_var, dim3(nb), dim3(kPT), 0, st, P, n, (const double*)part1, (int)nb, part2, avg);
     return hipGetLastError();
 }

@@ -134,7 +134,26 @@ def deep(kind: str, h: int, w: int, seed: int) -> np.ndarray:
     """A 16-bit image as the planar doubles a C caller of get_full_report_data
     may pass (value / 65535, src/interface.c:20-94): the 8-bit `kind` image
     scaled by 257 plus 8 bits of uniform noise.  float64 HxWx3 in [0, 1],
-    almost no value equal to any k/255.0."""
-    base = make(kind, h, w, seed).astype(np.float64) * 257.0
+    almost no value equal to any k/255.0.
+
+    Two suffixes give finite doubles outside [0, 1] that the reference still
+    reports on (no octree index out of bounds): `kind+neg` -- a rectangle
+    (rows H/4..H/2, columns W/3..2W/3) whose channels are -(2 x + 0.01), all
+    negative (rgb2hsv's v < 0: the black group), so the luma reaches -2;
+    `kind+spike` -- every 97th pixel of the odd columns (which downsample_rgb
+    at rate 2 never samples) set to 40.0 in red, so only the statistics, the
+    luma and the FFT see it."""
+    base_kind, _, mod = kind.partition("+")
+    base = make(base_kind, h, w, seed).astype(np.float64) * 257.0
     noise = uniform(h, w, seed + 7919).astype(np.float64)
-    return np.minimum(base + noise, 65535.0) / 65535.0
+    img = np.minimum(base + noise, 65535.0) / 65535.0
+    if mod == "neg":
+        sl = (slice(h // 4, h // 2), slice(w // 3, 2 * w // 3))
+        img[sl] = -(2.0 * img[sl] + 0.01)
+    elif mod == "spike":
+        red = img[:, 1::2, 0].reshape(-1)
+        red[::97] = 40.0
+        img[:, 1::2, 0] = red.reshape(h, -1)
+    elif mod:
+        raise ValueError(f"unknown deep modifier {mod!r}")
+    return img

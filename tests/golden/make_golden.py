@@ -74,6 +74,12 @@ PLANAR_CASES = [
     ("deep_motion_1201x1009_hsv36", "motion", 1201, 1009, 43, HSV36, None),
     ("deep_dominant_1024x1536", "dominant", 1024, 1536, 44, {}, None),
     ("deep_hblur_3000x4000", "hblur", 3000, 4000, 45, {}, None),
+    # round 5: finite doubles outside [0, 1] that the reference reports on --
+    # negative channels (luma down to -2) and spikes on pixels downsample_rgb
+    # does not sample (luma 12): the polar bins' fixed point follows the range
+    ("deep_structured_neg_600x800", "structured+neg", 600, 800, 46, {}, None),
+    ("deep_uniform_spike_700x900_ds2", "uniform+spike", 700, 900, 47, {"downsample_rate": 2}, None),
+    ("deep_hblur_neg_3000x4000", "hblur+neg", 3000, 4000, 48, HSV36, None),
 ]
 
 # get_blur_profile_visual (src/blur_profile.c:140-180) on a Blur_Profile whose

@@ -188,3 +188,15 @@ def test_free_full_report_ignores_foreign_pointers():
     null = ctypes.POINTER(Full_Report_Data)()
     lib.free_full_report(ctypes.byref(null))
     lib.phd_free_reports(None, 3)
+
+
+def test_column_run_lists_fit_the_default_grid_only():
+    """Host only: the compile-time column pass holds at most 256 run-list entries
+    per spectrum column.  The default 72 x 40 grid at 4000x3000 and config 5's
+    largest sizes fit; radius_partitions = 160 does not (that size takes the
+    runtime-plan FFT, tests/test_gpu_round5.py)."""
+    from photohive_dsp_amd.lib import lib
+    for h, w in ((3000, 4000), (4000, 6000), (6000, 4000), (4000, 3000)):
+        assert 0 < lib.phd_debug_col_runs_max(h, w, 40, 72) <= 256, (h, w)
+    assert lib.phd_debug_col_runs_max(3000, 4000, 160, 72) > 256
+    assert lib.phd_debug_col_runs_max(300, 4000, 40, 0) == -1

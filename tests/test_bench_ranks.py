@@ -1,7 +1,8 @@
 """bench.py's multi-rank path on the CPU: `python bench.py --gpus 2` with no
 torchrun environment starts the ranks itself (a torch.distributed.run child),
-every rank takes its shard of configs 2, 4 and 5 and one gloo all-gather
-merges the counters; rank 0 prints one JSON line with both ranks' images."""
+every rank takes its shard of configs 2, 4 and 5 and one gloo all_reduce
+(shard.merge_counters) merges the counters; rank 0 prints one JSON line with
+both ranks' images."""
 import json
 import os
 import subprocess
@@ -27,3 +28,24 @@ def test_bench_gpus2_spawns_ranks_and_merges_counters():
     sizes = shard.mixed_sizes(96, 5)
     assert d["config5"]["pixels"] == sum(h * w for h, w in sizes)
     assert d["config2"]["elapsed_max"] == 2.0                   # max over ranks (1 + rank)
+
+
+def test_every_roofline_prices_algorithmic_bytes():
+    """Every roofline object bench.py builds takes its bytes from
+    algorithmic_bytes, never from a literal byte formula."""
+    import ast
+    import re
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    tree = ast.parse(src)
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Assign) and any(isinstance(t, ast.Name) and t.id == "ab" for t in node.targets):
+            seg = ast.get_source_segment(src, node.value)
+            assert "algorithmic_bytes(" in seg, f"bench.py:{node.lineno}: ab = {seg}"
+    # no per-element byte constants left in the byte counts (the removed 18 H Wf bin map)
+    assert not re.search(r"\b18(\.0)? \* h", src)
+    sys.path.insert(0, ROOT)
+    import bench
+    h, w = 3000, 4000
+    assert bench.algorithmic_bytes("fft_cols", h, w) == 16 * h * (w // 2 + 1)
+    assert bench.algorithmic_bytes("blur_path", h, w) == 3 * h * w + 32 * h * (w // 2 + 1)
+    assert bench.algorithmic_bytes("report", h, w) == 9 * h * w + 32 * h * (w // 2 + 1)

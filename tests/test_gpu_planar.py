@@ -103,16 +103,23 @@ def test_planar_rejects_non_finite():
     assert "finite" in L.last_error()
 
 
-def test_planar_rejects_oversized_unsampled_value():
-    """downsample_rate 2: a huge finite value on a pixel downsample_rgb never
-    samples (odd column) reaches only the statistics and the FFT.  Its luma
-    breaks the polar bins' fixed-point bound (|pgm - avg| <= 1, bin_scale), so
-    the call is rejected with a message instead of returning wrapped sums."""
+def test_planar_unsampled_spike_and_overflowing_values():
+    """downsample_rate 2: a value on a pixel downsample_rgb never samples (odd
+    column) reaches only the statistics and the FFT.  A finite spike (40.0)
+    gets a report -- the polar bins' fixed-point scale follows the luma range
+    (the deep_*_spike fixture pins its values); a value whose power spectrum
+    overflows fp64 (1e300) is rejected with a message instead of infinite
+    bins."""
     phd, L = _phd()
     from photohive_dsp_amd import synth
     img = synth.deep("uniform", 400, 400, 2)
     ok = _call(img, {"downsample_rate": 2})
     assert ok is not None
-    img[11, 11, 0] = 1e300                            # column 11: not sampled at ds = 2 (x * 2)
+    img[11, 11, 0] = 40.0                             # column 11: not sampled at ds = 2 (x * 2)
+    spiked = _call(img, {"downsample_rate": 2})
+    assert spiked is not None
+    assert spiked.color_palette.quantities == ok.color_palette.quantities   # the palette never sees it
+    assert np.isfinite(np.array(spiked.blur_profile.bins)).all()
+    img[11, 11, 0] = 1e300
     assert _call(img, {"downsample_rate": 2}) is None
-    assert "luma" in L.last_error()
+    assert "too large" in L.last_error()

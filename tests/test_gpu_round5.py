@@ -1,0 +1,54 @@
+"""Round-5 GPU tests: two library lanes on eight HIP hardware queues in a fresh
+process (the bench's default configuration), and the compile-time size whose
+polar-bin table has too many runs per column for the column pass's run lists
+(the runtime-plan fallback) against the oracle."""
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import _phd, assert_report_matches
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_two_lanes_eight_hw_queues_fresh_process():
+    """GPU_MAX_HW_QUEUES=8 must be in the environment before HIP initialises,
+    so the batch runs in a child process: 32 device-resident 4000x3000 images
+    (uniform and structured), three two-lane calls and one one-lane call;
+    every report field is identical between them (S-bar and the palette's
+    h / s / v, fp64 sums whose atomics land in any order, within 1e-12)."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "lanes_hwq_child.py"), "32"],
+                       env=env, capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, (r.returncode, r.stderr[-3000:])
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["hw_queues"] == "8" and d["images"] == 32
+    assert d["n_diffs"] == 0, d["diffs"]
+
+
+def test_column_runs_fallback_4000x3000_against_oracle():
+    """radius_partitions = 160 at 4000x3000 gives spectrum columns of up to 265
+    polar-bin runs, more than the compile-time column pass holds (256): the
+    size takes the runtime-plan FFT.  Two calls (the second hits the cached
+    decision) both match the oracle."""
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    from oracle import oracle as orc
+    H, W = 3000, 4000
+    assert L.lib.phd_debug_col_runs_max(H, W, 160, 72) > 256
+    img = synth.make("structured", H, W, 31)
+    o = orc.report(img, fft_workers=8, radius_partitions=160)
+    g = dict(stats=o.stats, average_saturation=np.array(o.average_saturation),
+             valid_parents=o.valid_parents, palette_pct=o.palette_pct, palette_hsv=o.palette_hsv,
+             bins=o.bins, blur_angles=o.blur_angles, blur_mags=o.blur_mags,
+             angle_bin_size=np.array(o.angle_bin_size), radius_bin_size=np.array(o.radius_bin_size))
+    for _ in range(2):
+        rep = phd.get_report(img, radius_partitions=160)
+        assert_report_matches(rep, g)
