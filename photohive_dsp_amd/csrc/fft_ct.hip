@@ -230,8 +230,8 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
                     const double p1 = kWr * byte_of(rg[j][1], 3 * e) + kWg * byte_of(rg[j][1], 3 * e + 1) +
                                       kWb * byte_of(rg[j][1], 3 * e + 2);
                     z[e] = make_double2(p0, two ? p1 : 0.0);
-                    // the channel sums of get_rgb_statistics' means (the column pass's
-                    // DC bias), exact integers: the FFTs need nothing from K1
+                    // rsum (the blur-only path, which runs no K1): the channel sums
+                    // of the column pass's DC bias, exact integers
                     if (rsum) {                                   // uniform
                         cs[0] += byte_of(rg[j][0], 3 * e) + (two ? byte_of(rg[j][1], 3 * e) : 0);
                         cs[1] += byte_of(rg[j][0], 3 * e + 1) + (two ? byte_of(rg[j][1], 3 * e + 1) : 0);
@@ -302,74 +302,55 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     }
 }
 
-template <int H, int T, int CPB, int... Rs>
+template <int H, int T, int... Rs>
 struct ColK {
     using PL = Plan<H, T, 1, Rs...>;
     using L = typename PL::Last;
     static constexpr int R = Radices<Rs...>::count > 0 ? H / L::NB : 1;   // last radix
     static constexpr int NTW = tw_entries<1, Rs...>();
     static constexpr int P = (H + 1) / 2;                                 // row pairs
-    // CPB = flags: bits 0-1 columns per block (1 or 2); 4: no register
-    // prefetch (the step's tiles are loaded at its start, other blocks of the
-    // CU hide the latency); 8: bins summed with global atomics (no LDS bins)
-    // 32: pass 0 from registers (one column per block: thread b < H/R0 loads
-    // rows b + r H/R0 of the next column, runs its first butterfly on them and
-    // stores the outputs -- no LDS round trip for the raw column)
-    static constexpr int NC = CPB & 3;
-    static constexpr bool PF = !(CPB & 4);
-    static constexpr bool GB = (CPB & 8) != 0;
-    static constexpr bool P0R = (CPB & 32) != 0;
-    using PE = Peel<H, T, Rs...>;
-    static constexpr int NT = NC * T;                                     // block size
-    static constexpr int CR = (2 * NC * P + NT - 1) / NT;                 // load rounds
+    static constexpr int CR = (2 * P + T - 1) / T;                        // load rounds
     static constexpr int E = (H + T - 1) / T;                             // epilogue run per thread
-    // the run lists of the block's columns (ColRuns): kColRunsMax entries each,
-    // RPT per thread
+    // the run list of the block's column (ColRuns): kColRunsMax entries, RPT
+    // per thread
     static constexpr int RPT = (kColRunsMax + T - 1) / T;
-    // + per column its run list and one u64 slot per run (the bins are summed
-    // per run, then added to the image's bins column by column: no LDS array
-    // of all na x nr bins)
-    static size_t lds(int) {
-        return sizeof(double2) * (NC * H + NTW + kLogTab) + (sizeof(unsigned) + sizeof(unsigned long long)) * NC *
-                                                                kColRunsMax;
-    }
+    // the column, the twiddles, log_mant's table, the column's run list and
+    // one u64 slot per run (the bins are summed per run, then added to the
+    // image's bins column by column: no LDS array of all na x nr bins)
+    static constexpr size_t lds =
+        sizeof(double2) * (H + NTW + kLogTab) + (sizeof(unsigned) + sizeof(unsigned long long)) * kColRunsMax;
     static_assert(Radices<Rs...>::product == H, "plan");
-    // waves per SIMD of the launch bounds: one-column blocks are sized for two
-    // resident blocks per CU, one when the column and twiddles fill the LDS
-    static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
-    // 64: sized for three resident one-column blocks per CU (168 VGPRs; the
-    // LDS holds three 3000-row columns now that the bins are per run)
-    static constexpr int MINW = (CPB & 64) ? 3 : (CPB & 16) ? (3 * ((T + 63) / 64) + 3) / 4 : (NC == 1 ? (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2 : 1);
-    static_assert(NC == 1 || NC == 2, "columns per block");
-    static_assert(!P0R || (NC == 1 && PF && PE::NB <= T && Radices<Rs...>::count >= 2), "pass 0 from registers");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
+    // waves per SIMD of the launch bounds: sized for two resident blocks per
+    // CU, one when the column and twiddles fill the LDS
+    static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
+    static constexpr int MINW = (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2;
 };
 
-// Two columns per block: one column pair per step; threads [0, T) take column
-// 2kp, [T, 2T) column 2kp+1.  One column per block: blocks b, b^8, b^16, b^24
-// (same XCD) take the four columns of the same 128-byte lines (two tiles), so
-// each line is fetched once into that XCD's L2 (the grid is a multiple of 32).
-// one-column blocks are sized for two resident blocks per CU
-template <int H, int T, int CPB, int... Rs>
-__global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
+// One column per block: blocks b, b^8, b^16, b^24 (one XCD) take the four
+// columns of the same 128-byte lines (two tiles), so each line is fetched once
+// into that XCD's L2 (the grid is a multiple of 32).  A step's tiles are
+// loaded at its start; the other blocks of the CU hide the latency (round 3:
+// prefetching the next column into registers measured slower, it cost VGPRs).
+template <int H, int T, int... Rs>
+__global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
                                                      const unsigned* __restrict__ runs,
-                                                     const uint8_t* __restrict__ segidx, int rstride, int nbins,
+                                                     const uint8_t* __restrict__ segidx, int rstride,
                                                      unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums0, int width,
                                                      double* __restrict__ dbg, double bscale, int ablate_arg,
                                                      int nimg, long istride, long bstride, long fstride, long sstride) {
-    using K = ColK<H, T, CPB, Rs...>;
-    constexpr int NC = K::NC;
+    using K = ColK<H, T, Rs...>;
     const int ablate = PHD_ABL(ablate_arg);
     using L = typename K::L;
-    constexpr int R = K::R, NT = K::NT;
+    constexpr int R = K::R;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    double2* bufs = reinterpret_cast<double2*>(smem);         // [CPB][H]
-    double2* tw = bufs + NC * H;
+    double2* buf = reinterpret_cast<double2*>(smem);          // [H]
+    double2* tw = buf + H;
     double2* lt = tw + K::NTW;                                 // log_mant's table
-    unsigned long long* slots = reinterpret_cast<unsigned long long*>(lt + kLogTab);   // [NC][kColRunsMax]
-    unsigned* rbuf = reinterpret_cast<unsigned*>(slots + NC * kColRunsMax);         // [NC][kColRunsMax]
+    unsigned long long* sl = reinterpret_cast<unsigned long long*>(lt + kLogTab);   // [kColRunsMax]
+    unsigned* rl = reinterpret_cast<unsigned*>(sl + kColRunsMax);                   // [kColRunsMax]
     const int tid = threadIdx.x;
     // a batch: nimg images of one size, their intermediates, bin sums, max
     // partials and channel sums istride / bstride / fstride / sstride apart;
@@ -378,60 +359,29 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     unsigned long long* bin_sums = bin_sums0;
     double* fmax_part = fmax_part0;
     const unsigned long long* sums = sums0;
-    // NC == 1: blocks b, b^8, b^16, b^24 (one XCD) take the four columns of a
-    // 128-byte line (two tiles), so each line is fetched once into that L2
-    // NC == 2: blocks b, b^8 (one XCD) take the two tiles of a 128-byte line
-    const int quad = NC == 2 ? (int)((blockIdx.x >> 3) & 1) * 2 : (int)((blockIdx.x >> 3) & 3);
-    const int half = NC == 2 ? (tid >= T ? 1 : 0) : (quad & 1);   // column of the pair
-    const int ht = NC == 2 ? tid - half * T : tid;
-    double2* buf = bufs + (NC == 2 ? half * H : 0);
-    for (int i = tid; i < K::NTW; i += NT) tw[i] = twg[i];
-    for (int i = tid; i < NC * kColRunsMax; i += NT) slots[i] = 0ull;
-    log_table_init(lt, tid, NT);
+    // blocks b, b^8, b^16, b^24 (one XCD) take the four columns of a 128-byte
+    // line (two tiles), so each line is fetched once into that L2
+    const int quad = (int)((blockIdx.x >> 3) & 3);
+    const int half = quad & 1;                                 // column of the pair
+    for (int i = tid; i < K::NTW; i += T) tw[i] = twg[i];
+    for (int i = tid; i < kColRunsMax; i += T) sl[i] = 0ull;
+    log_table_init(lt, tid, T);
     const int kpn = (wf + 1) / 2;
     const size_t rs = (size_t)((4 * kpn + 7) & ~7);           // row-pair stride (ct_row_stride)
     const int nunit = (kpn + 1) / 2;                          // tile pairs (128-byte lines)
-    const int nlog = NC == 2 ? (int)gridDim.x / 2 : (int)gridDim.x / 4;
-    const int lblk = NC == 2 ? (int)((blockIdx.x >> 4) * 8 + (blockIdx.x & 7))
-                             : (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
+    const int nlog = (int)gridDim.x / 4;
+    const int lblk = (int)((blockIdx.x >> 5) * 8 + (blockIdx.x & 7));
     // a batch numbers its images' units one after the other: a block's range
     // may span the end of one image and the start of the next (small images)
     const long nall = (long)nimg * nunit;
     const int c0 = (int)(lblk * nall / nlog), c1 = (int)((lblk + 1) * nall / nlog);
-    // the column pair of step u (NC == 1: tile 2u or 2u+1; past the last tile
-    // the block re-reads the last one and idles)
+    // the column pair of step u (tile 2u or 2u+1; past the last tile the block
+    // re-reads the last one and idles)
     auto pair_at = [&](int u) { return min(2 * u + (quad >> 1), kpn - 1); };
-    // the tiles: element 4p + 2c + r is (row 2p + r, column 2kp + c).  NC == 2
-    // loads whole 64-B tiles (thread -> row pair tid/4, sub-element tid%4), CPB
-    // == 1 its column's 32-B half (row pair tid/2, row tid%2)
-    constexpr int PER = 2 * NC;                               // elements of one row pair a block loads
-    // raw 16-byte words: the loads land in the registers the LDS stores read
-    // (no moves, so nothing waits for them before the next step)
-    u32x4 pf[K::CR];
-    const int prow0 = tid / PER, psub = NC == 2 ? (tid & 3) : 2 * half + (tid & 1);
-#define PHD_COL_FETCH(kpv)                                                                  \
-    do {                                                                                    \
-        const u32x4* src_ = reinterpret_cast<const u32x4*>(inter) +                         \
-                            (size_t)prow0 * rs + (size_t)(kpv) * 4 + psub;                  \
-        _Pragma("unroll") for (int c = 0; c < K::CR; c++) {                                \
-            /* rows past the end re-read the last row pair (unused, no branch) */           \
-            const int pr_ = min(c * (NT / PER), K::P - 1 - prow0);                          \
-            pf[c] = src_[(size_t)pr_ * rs];                                                 \
-        }                                                                                   \
-    } while (0)
-    // K::P0R: thread ht < NB0 holds rows ht + r NB0 of its column (pass 0's inputs)
-    constexpr int R0 = K::PE::R, NB0 = K::PE::NB;
-    double2 p0v[1][K::P0R ? R0 : 1];
-    auto fetch0 = [&](int kpv) {
-        const double2* src = inter + ((size_t)kpv * 2 + half) * 2;
-        if (ht < NB0) {
-#pragma unroll
-            for (int r = 0; r < (K::P0R ? R0 : 1); r++) {
-                const int y = ht + r * NB0;
-                p0v[0][r] = src[(size_t)(y >> 1) * rs + (y & 1)];
-            }
-        }
-    };
+    // the tiles: element 4p + 2c + r is (row 2p + r, column 2kp + c); a thread
+    // loads its column's 32-B half of tiles (row pair tid/2, row tid%2), as raw
+    // 16-byte words that land in the registers the LDS stores read
+    const int prow0 = tid / 2, psub = 2 * half + (tid & 1);
     // (a block without units still runs one empty segment: its max partial and
     // bins are written as the one-image form always did)
     for (int seg = c0, im = c0 / nunit, first = 1; first || seg < c1; im++, first = 0) {
@@ -442,39 +392,31 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
     bin_sums = bin_sums0 + im * bstride;
     fmax_part = fmax_part0 + im * fstride;
     sums = sums0 + im * sstride;
-    if (K::P0R && u0 < un) fetch0(pair_at(u0));
-    else if (K::PF && u0 < un) PHD_COL_FETCH(pair_at(u0));
     double mx = 0.0;
     __syncthreads();
     for (int u = u0; u < un; u++) {
         const int kp = pair_at(u);
-        if (!K::PF) PHD_COL_FETCH(kp);
-        if constexpr (K::P0R) {
-            if (kp == 0 && 2 * (2 * u + (quad >> 1)) + half == 0 && ht < NB0) {   // block-uniform kp, col
-                // remove_dc_bias on the registers (see below)
-                const double n = (double)H * (double)width;
-                const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
-                                    (double)sums[2] / 255.0 / n) / 3.0;
-                const double dc = (double)width * avg;
-#pragma unroll
-                for (int r = 0; r < R0; r++) p0v[0][r].x -= dc;
-            }
-            if (!(ablate & 1)) K::PE::P0::compute(p0v, tw, ht);
-            K::PE::P0::store(buf, p0v, ht);
-        } else {
-            u32x4* dst = reinterpret_cast<u32x4*>(bufs + (NC == 2 ? ((psub >> 1) & 1) * H : 0) + 2 * prow0 +
-                                                  (psub & 1));
+        {
+            u32x4 pf[K::CR];
+            const u32x4* src = reinterpret_cast<const u32x4*>(inter) + (size_t)prow0 * rs + (size_t)kp * 4 + psub;
 #pragma unroll
             for (int c = 0; c < K::CR; c++) {
-                const int y = 2 * (prow0 + c * (NT / PER)) + (psub & 1);
-                if (((PER * K::P) % NT == 0 || tid + c * NT < PER * K::P) && (H % 2 == 0 || y < H))
-                    dst[c * 2 * (NT / PER)] = pf[c];
+                // rows past the end re-read the last row pair (unused, no branch)
+                const int pr = min(c * (T / 2), K::P - 1 - prow0);
+                pf[c] = src[(size_t)pr * rs];
+            }
+            u32x4* dst = reinterpret_cast<u32x4*>(buf + 2 * prow0 + (psub & 1));
+#pragma unroll
+            for (int c = 0; c < K::CR; c++) {
+                const int y = 2 * (prow0 + c * (T / 2)) + (psub & 1);
+                if (((2 * K::P) % T == 0 || tid + c * T < 2 * K::P) && (H % 2 == 0 || y < H))
+                    dst[c * T] = pf[c];
             }
         }
         const int col = 2 * (2 * u + (quad >> 1)) + half;
         const bool live = col < wf;                       // the phantom column of an odd wf idles
         // the column's bin runs (image-independent, ~0.3 KB per column; ColRuns)
-        // and the run holding this thread's first row ht * E: loaded now, stored
+        // and the run holding this thread's first row tid * E: loaded now, stored
         // to LDS after the FFT (a phantom column reads column 0's: its p are 1)
         unsigned rreg[K::RPT];
         int sidx;
@@ -483,14 +425,13 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
             const unsigned* rsrc = runs + (size_t)rc * rstride;
 #pragma unroll
             for (int k = 0; k < K::RPT; k++) {
-                const int e = ht + k * T;
+                const int e = tid + k * T;
                 rreg[k] = e < rstride ? rsrc[e] : 0u;
             }
-            sidx = segidx[(size_t)rc * T + ht];
+            sidx = segidx[(size_t)rc * T + tid];
         }
-        if (!K::P0R && K::PF && u + 1 < un && !(ablate & 4)) PHD_COL_FETCH(pair_at(u + 1));
         __syncthreads();
-        if (!K::P0R && kp == 0) {                         // block-uniform
+        if (kp == 0) {                                    // block-uniform
             // remove_dc_bias (src/blur_profile.c:233-238): a constant per image only
             // moves the row spectra's k = 0 column, by W * avg per row, with avg =
             // (Br + Bg + Bb) / 3 (src/interface.c:78) from K1's exact channel sums
@@ -499,25 +440,21 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                 const double avg = ((double)sums[0] / 255.0 / n + (double)sums[1] / 255.0 / n +
                                     (double)sums[2] / 255.0 / n) / 3.0;
                 const double dc = (double)width * avg;
-                for (int y = ht; y < H; y += T) buf[y].x -= dc;
+                for (int y = tid; y < H; y += T) buf[y].x -= dc;
             }
             __syncthreads();
         }
-        if constexpr (K::P0R) {
-            if (!(ablate & 1)) K::PE::RestPlan::all_but_last(buf, tw, ht);
-        } else {
-            if (!(ablate & 1)) K::PL::all_but_last(buf, tw, ht);
-        }
+        if (!(ablate & 1)) K::PL::all_but_last(buf, tw, tid);
         double2 v[L::ROUNDS][R];
         if (!(ablate & 16)) {
-            L::load(buf, v, ht);
-            L::compute(v, tw + K::PL::last_tw_offset, ht);
+            L::load(buf, v, tid);
+            L::compute(v, tw + K::PL::last_tw_offset, tid);
         }
         __syncthreads();                       // every thread has read its last-pass inputs
         double* lgb = reinterpret_cast<double*>(buf);   // p per spectrum row, 1 for p < 1 (log 0)
 #pragma unroll
         for (int q = 0; q < L::ROUNDS; q++) {
-            const int b = ht + q * T;
+            const int b = tid + q * T;
             if (L::active(b) && !(ablate & 16)) {
 #pragma unroll
                 for (int k = 0; k < R; k++) {
@@ -529,24 +466,20 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
                 }
             }
         }
-        // the next column's pass-0 inputs (p0v is free from here to the next step)
-        if (K::P0R && u + 1 < un && !(ablate & 4)) fetch0(pair_at(u + 1));
-        unsigned* rl = rbuf + (NC == 2 ? half * kColRunsMax : 0);   // the previous walk ended at a barrier
 #pragma unroll
         for (int k = 0; k < K::RPT; k++)
-            if (ht + k * T < kColRunsMax) rl[ht + k * T] = rreg[k];
+            if (tid + k * T < kColRunsMax) rl[tid + k * T] = rreg[k];
         __syncthreads();
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
-        unsigned long long* sl = slots + (NC == 2 ? half * kColRunsMax : 0);
-        if (!(ablate & 2)) walk_runs<K::E>(lgb, ht * K::E, H, rl, sidx, sl, bscale, lt);
+        if (!(ablate & 2)) walk_runs<K::E>(lgb, tid * K::E, H, rl, sidx, sl, bscale, lt);
         __syncthreads();
         // the column's run sums into the image's bins (a bin met by two runs of
         // a column gets two atomics); entries past the sentinel start at H
         if (!(ablate & 8)) {
 #pragma unroll
             for (int k = 0; k < K::RPT; k++) {
-                const int t = ht + k * T;
+                const int t = tid + k * T;
                 if (t < kColRunsMax && t < rstride) {
                     const unsigned e = rl[t];
                     const unsigned long long v = sl[t];
@@ -558,15 +491,14 @@ __global__ __launch_bounds__((CPB & 3) * T, (ColK<H, T, CPB, Rs...>::MINW)) void
             }
         }
     }
-#undef PHD_COL_FETCH
-    // block max -> one partial per block; non-zero bins -> the image's sums
+    // block max -> one partial per block
     mx = wave_max(mx);
-    double* red = reinterpret_cast<double*>(bufs);
+    double* red = reinterpret_cast<double*>(buf);
     if (lane_id() == 0) red[tid >> 6] = mx;
     __syncthreads();
     if (tid == 0) {
         double m = 0.0;
-        for (int w = 0; w < (NT + 63) / 64; w++) m = fmax(m, red[w]);
+        for (int w = 0; w < (T + 63) / 64; w++) m = fmax(m, red[w]);
         fmax_part[blockIdx.x] = m;
     }
     if (seg < c1) __syncthreads();                             // red (in the buffer) is reused
@@ -579,15 +511,19 @@ void allow_big_lds(K kernel) {
                               160 * 1024);
 }
 
+// a persistent FFT grid of `full` resident blocks for this call: all of them,
+// or (fft_blocks_per_cu) one per CU when the call runs split over two lanes
+int fft_grid(int full) {
+    const int bpc = fft_blocks_per_cu(), cus = num_cus();
+    return (bpc > 0 && full > bpc * cus) ? bpc * cus : full;
+}
+
 // resident blocks per CU x CUs (the persistent grids)
 template <typename K>
 int resident_grid(K kernel, int threads, size_t lds) {
     allow_big_lds(kernel);
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess || nb < 1) nb = 1;
-    // PHD_FFT_BPC (experiment): at most this many persistent blocks per CU
-    static const int cap = phd_knob("PHD_FFT_BPC") ? atoi(phd_knob("PHD_FFT_BPC")) : 0;
-    if (cap > 0 && nb > cap) nb = cap;
     return nb * num_cus();
 }
 
@@ -596,58 +532,34 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
                    const double2* tw, double2* inter, unsigned long long* rsum, hipStream_t st,
                    const uint8_t* const* imgs = nullptr, int nimg = 1, long istride = 0) {
     const size_t lds = RowK<W, T, Rs...>::lds;
-    static const int grid = [&] {
-        const int g = resident_grid(k_rows_ct<W, T, Rs...>, T, lds) / 32 * 32;   // schedule needs % 32
-        return g > 32 ? g : 32;
-    }();
+    static const int full = resident_grid(k_rows_ct<W, T, Rs...>, T, lds);
+    const int g = fft_grid(full) / 32 * 32;                   // schedule needs % 32
+    const int grid = g > 32 ? g : 32;
     phd_launch((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
-                       g_ablate, rsum, imgs, nimg, istride);
+               g_ablate, rsum, imgs, nimg, istride);
     return hipGetLastError();
 }
 
-// column-pass LDS bytes of a plan (CPB flag 64: the LDS-DMA form)
-template <int H, int T, int CPB, int... Rs>
-size_t cols_lds(int nbins) {
-    return ColK<H, T, CPB, Rs...>::lds(nbins);
-}
-
-template <int H, int T, int CPB, int... Rs>
-int cols_grid(int, int nbins) {
-    int g = resident_grid(k_cols_ct<H, T, CPB, Rs...>, (CPB & 3) * T, ColK<H, T, CPB, Rs...>::lds(nbins));
-    if ((CPB & 3) == 2) {
-        g = g / 16 * 16;                                    // XCD pairs b, b^8
-        return g < 16 ? 16 : g;
-    }
-    g = g / 32 * 32;                                        // XCD quads b, b^8, b^16, b^24
+// the resident grid (the most blocks of any call: the max-partial records)
+template <int H, int T, int... Rs>
+int cols_grid() {
+    const int g = resident_grid(k_cols_ct<H, T, Rs...>, T, ColK<H, T, Rs...>::lds) / 32 * 32;   // XCD quads
     return g < 32 ? 32 : g;
 }
 
-template <int H, int T, int CPB, int... Rs>
+template <int H, int T, int... Rs>
 hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, unsigned long long* bin_sums,
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st, int nimg = 1, long istride = 0, long bstride = 0, long fstride = 0,
                    long sstride = 0) {
-    const size_t lds = cols_lds<H, T, CPB, Rs...>(0);
-    const int grid = cols_grid<H, T, CPB, Rs...>(wf, 0);
-    phd_launch((k_cols_ct<H, T, CPB, Rs...>), dim3(grid), dim3((CPB & 3) * T), lds, st, inter, wf, cb.runs, cb.seg,
-               cb.rstride, 0,
-               bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg, istride,
-               bstride, fstride, sstride);
+    static const int full = cols_grid<H, T, Rs...>();
+    const int g = fft_grid(full) / 32 * 32;
+    const int grid = g < 32 ? 32 : g;
+    phd_launch((k_cols_ct<H, T, Rs...>), dim3(grid), dim3(T), ColK<H, T, Rs...>::lds, st, inter, wf, cb.runs,
+               cb.seg, cb.rstride, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg,
+               istride, bstride, fstride, sstride);
     return hipGetLastError();
 }
-
-// the selected variant of length n, else variant 0
-#define PHD_PICK(LIST, n, rows, BODY)                                          \
-    do {                                                                       \
-        const int want_ = ct_variant(rows);                                    \
-        bool have_ = false;                                                    \
-        _Pragma("clang diagnostic push")                                       \
-        LIST(PHD_HAVE)                                                         \
-        _Pragma("clang diagnostic pop")                                        \
-        const int v_ = have_ ? want_ : 0;                                      \
-        LIST(BODY)                                                             \
-    } while (0)
-#define PHD_HAVE(N, V, T, ...) if (n_ == N && V == want_) have_ = true;
 
 // log_mant over an array (tests: its accuracy against the host's log)
 __global__ __launch_bounds__(256) void k_log_mant(const double* __restrict__ x, double* __restrict__ y, long n) {
@@ -666,62 +578,48 @@ hipError_t launch_log_mant(const double* x, double* y, long n, hipStream_t st) {
     return hipGetLastError();
 }
 
-int ct_variant(bool rows) {
-    static const int vr = phd_knob("PHD_CT_ROWS_VARIANT") ? atoi(phd_knob("PHD_CT_ROWS_VARIANT")) : 0;
-    static const int vc = phd_knob("PHD_CT_COLS_VARIANT") ? atoi(phd_knob("PHD_CT_COLS_VARIANT")) : 0;
-    return rows ? vr : vc;
-}
-
 bool ct_rows_plan(int w, std::vector<int>* radices) {
-    const int n_ = w;
-#define PHD_X(N, V, T, ...)                                          \
-    if (n_ == N && V == v_) {                                        \
-        if (radices) *radices = std::vector<int>{__VA_ARGS__};       \
-        return true;                                                 \
+#define PHD_X(N, T, ...)                                       \
+    if (w == N) {                                              \
+        if (radices) *radices = std::vector<int>{__VA_ARGS__}; \
+        return true;                                           \
     }
-    PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
+    PHD_CT_ROWS(PHD_X)
 #undef PHD_X
     return false;
 }
 
-template <int CPB, int... Rs>
-std::vector<int> col_radices() { return std::vector<int>{Rs...}; }
-
 bool ct_cols_plan(int h, std::vector<int>* radices) {
-    const int n_ = h;
-#define PHD_X(N, V, T, ...)                                          \
-    if (n_ == N && V == v_) {                                        \
-        if (radices) *radices = col_radices<__VA_ARGS__>();          \
-        return true;                                                 \
+#define PHD_X(N, T, ...)                                       \
+    if (h == N) {                                              \
+        if (radices) *radices = std::vector<int>{__VA_ARGS__}; \
+        return true;                                           \
     }
-    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+    PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return false;
 }
 
 int fft_cols_ct_threads(int h) {
-    const int n_ = h;
-#define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) return T;
-    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+#define PHD_X(N, T, ...) \
+    if (h == N) return T;
+    PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return 0;
 }
 
-size_t fft_cols_ct_lds(int h, int nbins) {
-    const int n_ = h;
-#define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) return cols_lds<N, T, __VA_ARGS__>(nbins);
-    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+size_t fft_cols_ct_lds(int h) {
+#define PHD_X(N, T, ...) \
+    if (h == N) return ColK<N, T, __VA_ARGS__>::lds;
+    PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return 0;
 }
 
-int fft_cols_ct_blocks(int height, int wf, int nbins) {
-    const int n_ = height;
-#define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) return cols_grid<N, T, __VA_ARGS__>(wf, nbins);
-    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+int fft_cols_ct_blocks(int h) {
+#define PHD_X(N, T, ...) \
+    if (h == N) return cols_grid<N, T, __VA_ARGS__>();
+    PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return 0;
 }
@@ -729,10 +627,9 @@ int fft_cols_ct_blocks(int height, int wf, int nbins) {
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
                               const double* k255, const double2* tw, double2* inter, hipStream_t st,
                               unsigned long long* rsum) {
-    const int n_ = width;
-#define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, rsum, st);
-    PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
+#define PHD_X(N, T, ...) \
+    if (width == N) return rows_ct<N, T, __VA_ARGS__>(img, height, sums, k255, tw, inter, rsum, st);
+    PHD_CT_ROWS(PHD_X)
 #undef PHD_X
     return hipErrorInvalidValue;
 }
@@ -740,12 +637,11 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 hipError_t launch_fft_rows_ct_batch(const uint8_t* const* d_imgs, int n, int height, int width, const double* k255,
                                     const double2* tw, double2* inter, long inter_stride, hipStream_t st) {
     if (n < 1 || ((height + 1) / 2) % 4 != 0) return hipErrorInvalidValue;   // whole line groups per image
-    const int n_ = width;
-#define PHD_X(N, V, T, ...)                                                                                  \
-    if (n_ == N && V == v_)                                                                                  \
+#define PHD_X(N, T, ...)                                                                              \
+    if (width == N)                                                                                   \
         return rows_ct<N, T, __VA_ARGS__>(nullptr, height, nullptr, k255, tw, inter, nullptr, st, d_imgs, n, \
                                           inter_stride);
-    PHD_PICK(PHD_CT_ROWS, n_, true, PHD_X);
+    PHD_CT_ROWS(PHD_X)
 #undef PHD_X
     return hipErrorInvalidValue;
 }
@@ -755,12 +651,11 @@ hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int
                                     double* fmax_part, long fmax_stride, const double2* tw,
                                     const unsigned long long* sums, long sums_stride, hipStream_t st) {
     if (n < 1) return hipErrorInvalidValue;
-    const int n_ = height;
-#define PHD_X(N, V, T, ...)                                                                                    \
-    if (n_ == N && V == v_)                                                                                    \
+#define PHD_X(N, T, ...)                                                                                       \
+    if (height == N)                                                                                           \
         return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, nullptr, st, n, \
                                           inter_stride, bin_stride, fmax_stride, sums_stride);
-    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+    PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return hipErrorInvalidValue;
 }
@@ -768,11 +663,10 @@ hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const ColBins& cb,
                               unsigned long long* bin_sums, double* fmax_part, const double2* tw,
                               const unsigned long long* sums, double* dbg, hipStream_t st) {
-    const int n_ = height;
-#define PHD_X(N, V, T, ...) \
-    if (n_ == N && V == v_) \
+#define PHD_X(N, T, ...) \
+    if (height == N)     \
         return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, dbg, st);
-    PHD_PICK(PHD_CT_COLS, n_, false, PHD_X);
+    PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return hipErrorInvalidValue;
 }

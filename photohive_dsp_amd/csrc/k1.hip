@@ -61,17 +61,19 @@ __device__ __forceinline__ int code_idx(int kmx, int kd) {
 constexpr int kCellBytes = 24;   // {u64 count word, f64 sum h, f64 sum s}
 
 // LDS carve (bytes).
+constexpr int kDq = 128;         // deferred-pixel queue entries per wave (u16 chunk offsets)
+
 struct LVar {
-    int cells, code, k255, inv, red, rcell, cg, seg, r255, rmx, gacc, end;
+    int cells, code, k255, red, dq, rcell, cg, seg, r255, rmx, gacc, end;
 };
-__host__ __device__ inline LVar l_var(int tl, int ncell, int cshift, int code_bytes, bool k255 = true) {
+__host__ __device__ inline LVar l_var(int tl, int ncell, int cshift, int code_bytes) {
     LVar v;
     v.cells = 0;                                                    // (ncell + 1) << cshift cells
     v.code = (kCellBytes * ((ncell + 1) << cshift) + 15) & ~15;     // code_bytes u8
     v.k255 = (v.code + code_bytes + 15) & ~15;                      // 256 f64: k / 255.0 (deferred pixels)
-    v.inv = v.k255 + (k255 ? 2048 : 0);                             // 256 K1Inv (16 B)
-    v.red = v.inv + 256 * (int)sizeof(K1Inv);                       // 16 waves x 8 u64
-    v.rcell = v.red + 1024;                                         // ncell u32: the run's cell counts
+    v.red = v.k255 + 2048;                                          // 16 waves x 8 u64
+    v.dq = v.red + 1024;                                            // 16 waves x kDq u16: deferred pixels
+    v.rcell = v.dq + 16 * kDq * 2;                                  // ncell u32: the run's cell counts
     v.cg = v.rcell + 4 * ncell;                                     // tl u32: the chunk's group counts
     v.seg = v.cg + 4 * tl;                                          // tl u32: the run's group counts
     v.r255 = v.seg + 4 * tl;                                        // tl u32: the run's #(kmax == 255)
@@ -113,10 +115,9 @@ struct CellRun {
 
 // 4 pixels (one dwordx3): moments, then each pixel classified and counted;
 // bit i of the result = pixel i deferred.
-template <bool TRI, bool SMALL, bool RT, bool MERGE = false>
+template <bool TRI, bool SMALL, bool MERGE>
 __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
                                              const unsigned char* __restrict__ code8,
-                                             const K1Inv* __restrict__ inv,
                                              unsigned char* __restrict__ cells, int cshift, int copy,
                                              const K1Grid& G, CellRun* run = nullptr, unsigned* same = nullptr) {
     const u16x2 one = {1, 1};
@@ -159,10 +160,10 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
-        // RT: the LDS table (two more LDS reads per pixel); else the VALU
-        // (measured faster: 40 against 46 us per image, the LDS is the busier)
-        ekd[i] = RT ? inv[kd > 1 ? kd : 1] : k1_inv_valu(kd > 1 ? kd : 1);
-        ikm[i] = RT ? inv[kmx > 1 ? kmx : 1].inv : k1_inv_valu(kmx > 1 ? kmx : 1).inv;
+        // from the VALU (round 4: an LDS table of reciprocals measured slower,
+        // 46 against 40 us per image -- the LDS is the busier pipe)
+        ekd[i] = k1_inv_valu(kd > 1 ? kd : 1);
+        ikm[i] = k1_inv_valu(kmx > 1 ? kmx : 1).inv;
     }
     unsigned def = 0;
 #pragma unroll
@@ -198,13 +199,14 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
     return def;
 }
 
-// MG: 0 every pixel's atomics; 1 per-thread cell runs (CellRun); 2 cell runs
-// for the next chunk when more than a fifth of this chunk's sampled 4-pixel
-// groups (each thread's first) lie in one cell, else per pixel -- flat images
-// (SURVEY 8(d) row 2(b)'s blurred structured ones: 81 % of groups) pay for
-// the runs' selects, noise does not.
-template <int KT, bool TRI, bool SMALL, int MINW = 4, bool LEAN = false, bool RT = false, int MG = 0>
-__global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restrict__ imgs, long npix, int nchunks,
+// Per-thread cell runs (CellRun) for the next chunk when more than a fifth of
+// this chunk's sampled 4-pixel groups (each thread's first) lie in one cell,
+// else every pixel's atomics -- flat images (SURVEY 8(d) row 2(b)'s blurred
+// structured ones: 81 % of groups) pay for the runs' selects, noise does not
+// (round 4: runs always 43.8 against 40.6 us on noise, never 80 against 48
+// on hblur).
+template <int KT, bool TRI, bool SMALL>
+__global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict__ imgs, long npix, int nchunks,
                                                long nitems, GridParams gp, K1Grid G,
                                                const ClassTables* __restrict__ tabs,
                                                const double* __restrict__ k255g, PaletteDev out, long a_stride,
@@ -217,15 +219,13 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
     constexpr int kT = KT, kG = kChunk / (4 * KT);              // threads; 4-pixel groups per thread per chunk
     static_assert(kG == 4 || kG == 8, "K1 tile");
     const int tl = gp.tl, ncell = G.ncell;
-    const LVar V = l_var(tl, ncell, cshift, code_bytes<TRI>(), MINW <= 4);
+    const LVar V = l_var(tl, ncell, cshift, code_bytes<TRI>());
     unsigned char* cells = smem + V.cells;
     unsigned char* code8 = smem + V.code;
-    K1Inv* inv = reinterpret_cast<K1Inv*>(smem + V.inv);
-    // the three-block form (MINW 6) has no LDS k / 255 table: k1_exact divides
-    double* k255 = MINW > 4 ? nullptr : reinterpret_cast<double*>(smem + V.k255);
+    double* k255 = reinterpret_cast<double*>(smem + V.k255);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + V.red);
-    // MG 2: the two chunk-parity vote counters, in the unused slot 7 of waves 0
-    // and 1's flush records (vote[0], vote[16])
+    // the two chunk-parity vote counters, in the unused slot 7 of waves 0 and
+    // 1's flush records (vote[0], vote[16])
     unsigned* vote = reinterpret_cast<unsigned*>(red + 7);
     int merge = 0, vpar = 0;                                    // block-uniform
     unsigned* rcell = reinterpret_cast<unsigned*>(smem + V.rcell);
@@ -239,10 +239,7 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
         const uint4* src = reinterpret_cast<const uint4*>(TRI ? tabs->code_tri : tabs->code8);
         uint4* dst = reinterpret_cast<uint4*>(code8);
         for (int i = tid; i < code_bytes<TRI>() / 16; i += kT) dst[i] = src[i];
-        if (k255)
-            for (int i = tid; i < 256; i += kT) k255[i] = k255g[i];
-        for (int k = tid; k < 256; k += kT)        // as k1_inv_init: correctly rounded quotients
-            inv[k] = k ? K1Inv{1.0 / (double)k, 1.0f / (float)k, 0u} : K1Inv{0.0, 0.0f, 0u};
+        for (int i = tid; i < 256; i += kT) k255[i] = k255g[i];
         unsigned* z = reinterpret_cast<unsigned*>(smem);
         for (int i = tid; i < V.code / 4; i += kT) z[i] = 0u;                        // cells
         for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;           // run records
@@ -256,69 +253,34 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
 
     const long full_end = npix & ~3L;
     int img = (int)(it0 / nchunks), c = (int)(it0 - (long)img * nchunks);
-    const uint8_t* ip = imgs[img];
-    unsigned w[kG][3];
-    // byte offsets within an image fit 32 bits (npix <= 120 MP, utilities.c:12)
-    auto issue = [&](const uint8_t* p, int cc) {
-        const long base = (long)cc * kChunk;
-        const unsigned off0 = (unsigned)(3 * (base + 4L * tid));
-        if (base + kChunk <= full_end) {                          // block-uniform
-#pragma unroll
-            for (int st = 0; st < kG; st++) {
-                gu32t* q = (gu32t*)(p + off0 + 12u * kT * st);
-                w[st][0] = q[0];
-                w[st][1] = q[1];
-                w[st][2] = q[2];
-            }
-        } else {
-#pragma unroll
-            for (int st = 0; st < kG; st++) {
-                // a group not wholly inside the image reads pixel 0 (masked below)
-                const bool ok = base + 4L * tid + 4L * kT * st < full_end;
-                gu32t* q = (gu32t*)(p + (ok ? off0 + 12u * kT * st : 0u));
-                w[st][0] = ok ? q[0] : 0u;
-                w[st][1] = ok ? q[1] : 0u;
-                w[st][2] = ok ? q[2] : 0u;
-            }
-        }
-    };
-    if (!LEAN) issue(ip, c);
     Mom m{0, 0, 0, 0, 0, 0};
     int seg_c0 = c;
     long seg_it0 = it0;
     for (long it = it0; it < it1; it++) {
         const long base = (long)c * kChunk;
-        unsigned cw[kG][3];
-        if (!LEAN) {
-#pragma unroll
-            for (int st = 0; st < kG; st++) {
-                cw[st][0] = w[st][0];
-                cw[st][1] = w[st][1];
-                cw[st][2] = w[st][2];
-            }
-        }
         const int cimg = img, cc = c;
         if (++c == nchunks) {
             c = 0;
             img++;
         }
         const bool more = it + 1 < it1;
-        if (more) {
-            if (img != cimg) ip = imgs[img];
-            if (!LEAN) issue(ip, c);
-        }
         const uint8_t* cip = imgs[cimg];
         unsigned emask = 0;                                       // deferred pixels (bit 4 st + i)
-        if constexpr (LEAN) {
+        {
             // one group (4 pixels) ahead only and the group loop not unrolled:
             // ~100 VGPRs without spills where the whole next chunk in registers
             // took 128 and spilled; the other waves of the CU hide the loads
+            // (groups past the image end read pixel 0, masked below)
+            const bool full = base + kChunk <= full_end;          // block-uniform: no group past the end
             auto ld = [&](int st, unsigned& x0, unsigned& x1, unsigned& x2) {
-                const bool ok = base + 4L * tid + 4L * kT * st < full_end;
+                // always a valid address, so the loads are unconditional (a
+                // guarded load became an exec-masked branch per word)
+                const bool ok = full || base + 4L * tid + 4L * kT * st < full_end;
                 gu32t* q = (gu32t*)(cip + (ok ? (unsigned)(3 * (base + 4L * tid)) + 12u * kT * st : 0u));
-                x0 = ok ? q[0] : 0u;
-                x1 = ok ? q[1] : 0u;
-                x2 = ok ? q[2] : 0u;
+                const unsigned l0 = q[0], l1 = q[1], l2 = q[2];
+                x0 = ok ? l0 : 0u;
+                x1 = ok ? l1 : 0u;
+                x2 = ok ? l2 : 0u;
             };
             unsigned a0, a1, a2;
             ld(0, a0, a1, a2);
@@ -330,8 +292,8 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
                 for (int st = 0; st < kG; st++) {
                     unsigned n0 = 0, n1 = 0, n2 = 0;
                     if (st + 1 < kG) ld(st + 1, n0, n1, n2);
-                    emask |= k1_group<TRI, SMALL, RT, M>(a0, a1, a2, m, code8, inv, cells, cshift, copy, G, &run,
-                                                         (MG == 2 && st == 0) ? &same0 : nullptr)
+                    emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, cells, cshift, copy, G, &run,
+                                                     st == 0 ? &same0 : nullptr)
                              << (4 * st);
                     a0 = n0;
                     a1 = n1;
@@ -343,17 +305,10 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
                     cell_add(cells, run.cell, cshift, copy, q);
                 }
             };
-            if (MG == 1 || (MG == 2 && merge)) loop(std::true_type{});
+            if (merge) loop(std::true_type{});
             else loop(std::false_type{});
-            if constexpr (MG == 2) {
-                const unsigned long long b = __ballot(same0);
-                if (lane_id() == 0) atomicAdd(&vote[16 * vpar], (unsigned)__popcll(b));
-            }
-        } else {
-#pragma unroll
-            for (int st = 0; st < kG; st++)
-                emask |= k1_group<TRI, SMALL, RT>(cw[st][0], cw[st][1], cw[st][2], m, code8, inv, cells, cshift, copy, G)
-                         << (4 * st);
+            const unsigned long long b = __ballot(same0);
+            if (lane_id() == 0) atomicAdd(&vote[16 * vpar], (unsigned)__popcll(b));
         }
         const bool last_chunk = base + kChunk >= npix;            // block-uniform
         if (last_chunk && tid == 0) {
@@ -364,32 +319,60 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
                 m.qr += kr * kr; m.qg += kg * kg; m.qb += kb * kb;
                 const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
                 const int code = code8[code_idx<TRI>(kmx, kmx - kmn)];
-                K1Px px = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kmx - kmn, code, inv[kmx - kmn > 1 ? kmx - kmn : 1],
-                                          inv[kmx > 1 ? kmx : 1].inv, G);
+                K1Px px = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kmx - kmn, code,
+                                          k1_inv_valu(kmx - kmn > 1 ? kmx - kmn : 1),
+                                          k1_inv_valu(kmx > 1 ? kmx : 1).inv, G);
                 if (px.cell == ncell) px = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
                 cell_add(cells, px.cell, cshift, copy, px);
             }
         }
         // deferred pixels (a non-special hue exactly on a half-bin boundary,
-        // ~1.7 % of uniform pixels): the thread redoes its own in fp64, re-reading
-        // the pixel from global memory (L2-resident: its chunk was just loaded)
-        // instead of keeping the chunk's words live through the classification
-        while (emask) {
-            const int bt = __ffs(emask) - 1;
-            emask &= emask - 1;
-            const int gst = bt >> 2, pi = bt & 3;
-            const uint8_t* q = cip + 3 * (base + 4L * tid + 4L * kT * gst + pi);
-            const int kr = q[0], kg = q[1], kb = q[2];
-            const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
-            const K1Px px = k1_exact(kr, kg, kb, code8[code_idx<TRI>(kmx, kmx - kmn)], gp.Lh, k255, G);
-            cell_add(cells, px.cell, cshift, copy, px);
+        // ~1.7 % of uniform pixels, ~35 per wave and chunk) are redone in fp64 by
+        // the whole wave: each lane queues its own (chunk offsets, this wave's LDS
+        // queue), then every lane takes one, re-reading the pixel from global
+        // memory (L2-resident: its chunk was just loaded).  One pass of the fp64
+        // path per <= kDq deferred pixels of the wave, where each lane redoing its
+        // own ran it as often as the wave's busiest lane had pixels (~3 times).
+        {
+            unsigned short* dq = reinterpret_cast<unsigned short*>(smem + V.dq) + (tid >> 6) * kDq;
+            const int lane = lane_id();
+            while (true) {                                        // wave-uniform
+                const int cnt = __popc(emask);
+                int incl = cnt;                                   // inclusive scan over the wave
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += y;
+                }
+                const int total = __shfl(incl, 63, 64);
+                if (total == 0) break;
+                int off = incl - cnt;
+                while (emask && off < kDq) {                      // what fits this round
+                    const int bt = __ffs(emask) - 1;
+                    emask &= emask - 1;
+                    dq[off++] = (unsigned short)(4 * tid + 4 * kT * (bt >> 2) + (bt & 3));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int k = lane; k < min(total, kDq); k += 64) {
+                    const uint8_t* q = cip + 3 * (base + (long)dq[k]);
+                    const int kr = q[0], kg = q[1], kb = q[2];
+                    const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
+                    const K1Px px = k1_exact(kr, kg, kb, code8[code_idx<TRI>(kmx, kmx - kmn)], gp.Lh, k255, G);
+                    cell_add(cells, px.cell, cshift, copy, px);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();                  // the queue is read before it is refilled
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
         }
         const long pad = base + kChunk - full_end;                // zero pixels of masked groups
         if (pad > 0 && tid == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(cells + kCellBytes * (zcell << cshift)),
                       (unsigned long long)(-pad));
         __syncthreads();
-        if constexpr (MG == 2) merge = 5 * vote[16 * vpar] > (unsigned)kT;   // the next chunk's mode
+        merge = 5 * vote[16 * vpar] > (unsigned)kT;              // the next chunk's mode
         // fold the chunk's count words: one thread per cell sums its C copies;
         // the run's cell counts, the chunk's group counts, per-group sum kmax / n255
         for (int q = tid; q <= ncell; q += kT) {
@@ -409,10 +392,8 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
             }
         }
         __syncthreads();
-        if constexpr (MG == 2) {
-            if (tid == 0) vote[16 * vpar] = 0u;                        // read by every thread before this barrier
-            vpar ^= 1;
-        }
+        if (tid == 0) vote[16 * vpar] = 0u;                      // read by every thread before this barrier
+        vpar ^= 1;
         unsigned short* chunk_out =
             reinterpret_cast<unsigned short*>(reinterpret_cast<char*>(out.chunk_hist) + cimg * h_stride) +
             (long)cc * tl;
@@ -497,21 +478,20 @@ __global__ __launch_bounds__(KT, MINW) void k_k1t(const uint8_t* const* __restri
     }
 }
 
-template <int KT, bool TRI, int MINW = 4, bool LEAN = false, bool RT = false, int MG = 0>
+template <int KT, bool TRI>
 void launch_form(int grid, size_t lds, hipStream_t st, const uint8_t* const* d_imgs, long npix, int nchunks,
                  long nitems, const GridParams& gp, const K1Grid& G, const ClassTables* tabs, const double* k255,
                  const PaletteDev& out0, long a_stride, long h_stride, int cshift) {
     if (G.small_c)
-        phd_launch((k_k1t<KT, TRI, true, MINW, LEAN, RT, MG>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
-                   gp, G, tabs, k255, out0, a_stride, h_stride, cshift);
+        phd_launch((k_k1t<KT, TRI, true>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
+                   k255, out0, a_stride, h_stride, cshift);
     else
-        phd_launch((k_k1t<KT, TRI, false, MINW, LEAN, RT, MG>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems,
-                   gp, G, tabs, k255, out0, a_stride, h_stride, cshift);
+        phd_launch((k_k1t<KT, TRI, false>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems, gp, G,
+                   tabs, k255, out0, a_stride, h_stride, cshift);
 }
 
 constexpr int kLds1 = 158 * 1024;   // one block per CU
 constexpr int kLds2 = 79 * 1024;    // two blocks per CU
-constexpr int kLds3 = 160 * 1024 / 3 - 256;   // three blocks per CU
 
 }  // namespace
 
@@ -556,97 +536,40 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     static const bool attr = [] {
         const void* fs[] = {(const void*)k_k1t<1024, false, true>, (const void*)k_k1t<1024, false, false>,
                             (const void*)k_k1t<1024, true, true>,  (const void*)k_k1t<1024, true, false>,
-                            (const void*)k_k1t<512, true, true>,   (const void*)k_k1t<512, true, false>,
-                            (const void*)k_k1t<512, true, true, 6, true>, (const void*)k_k1t<512, true, false, 6, true>,
-                            (const void*)k_k1t<512, true, true, 4, true>, (const void*)k_k1t<512, true, false, 4, true>,
-                            (const void*)k_k1t<512, true, true, 4, true, true>,
-                            (const void*)k_k1t<512, true, false, 4, true, true>,
-                            (const void*)k_k1t<512, true, true, 4, true, false, 1>,
-                            (const void*)k_k1t<512, true, false, 4, true, false, 1>,
-                            (const void*)k_k1t<512, true, true, 4, true, false, 2>,
-                            (const void*)k_k1t<512, true, false, 4, true, false, 2>,
-                            (const void*)k_k1t<1024, true, true, 4, true, false, 2>,
-                            (const void*)k_k1t<1024, true, false, 4, true, false, 2>,
-                            (const void*)k_k1t<1024, false, true, 4, true, false, 2>,
-                            (const void*)k_k1t<1024, false, false, 4, true, false, 2>};
+                            (const void*)k_k1t<512, true, true>,   (const void*)k_k1t<512, true, false>};
         for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
     (void)attr;
     // the two-block form runs a chunk in ~1.9x the time of the one-block form
     // (half a CU each): it wins when it has at least ~2 chunks per block, not
-    // for a single image's 732 chunks where its last chunks form the tail
+    // for a single image's 732 chunks where its last chunks form the tail.
+    // Measured and removed (round 4): three 512-thread
+    // blocks per CU (44.9 against 40.9 us per image), reciprocals from an LDS
+    // table (45.7), the whole next chunk prefetched into registers (spills).
     const long cus = num_cus();
-    // timing experiments (PHD_K1_FORM): 3 = three 512-thread blocks per CU, one
-    // lane copy of the cells, no k / 255 table (53 KiB each), 6 waves per SIMD
-    // (measured slower: 44.9 against 40.9 us per image before the reciprocal
-    // table); 5 = the two-block form with the whole next chunk prefetched into
-    // registers (the round-3 loop: 128 VGPRs, spills)
-    static const int form = phd_knob("PHD_K1_FORM") ? atoi(phd_knob("PHD_K1_FORM")) : 0;
-    const size_t lds3 = (size_t)l_var(gp.tl, ncell, 0, code_bytes<true>(), false).end;
-    if (form == 3 && cshift2 >= 0 && lds3 <= (size_t)kLds3) {
-        const int grid = (int)std::min<long>(nitems, 3 * cus);
-        launch_form<512, true, 6, true>(grid, lds3, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                        a_stride, h_stride, 0);
-        return hipGetLastError();
-    }
-    if (form == 7 && cshift2 >= 0) {                         // the two-block form with per-thread cell runs
-        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
-        const int grid = (int)std::min<long>(nitems, 2 * cus);
-        launch_form<512, true, 4, true, false, 1>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
-                                                  k255, out0, a_stride, h_stride, cshift2);
-        return hipGetLastError();
-    }
-    if (form == 6 && cshift2 >= 0) {                         // the two-block form with the LDS reciprocal table
-        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
-        const int grid = (int)std::min<long>(nitems, 2 * cus);
-        launch_form<512, true, 4, true, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                              a_stride, h_stride, cshift2);
-        return hipGetLastError();
-    }
-    if (form == 5 && cshift2 >= 0) {
-        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
-        const int grid = (int)std::min<long>(nitems, 2 * cus);
-        launch_form<512, true, 4, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                         a_stride, h_stride, cshift2);
-        return hipGetLastError();
-    }
-    const bool two = cshift2 >= 0 && form != 1 &&            // PHD_K1_FORM=1: the one-block form (experiment)
-                     19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus);
+    const bool two = cshift2 >= 0 && 19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus);
     if (two) {                                            // two 512-thread blocks per CU
         const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
-        // with two lanes, one block per CU: the other half of each CU stays free
-        // for the other lane's FFT blocks (k1_blocks_per_cu)
+        // on a call split over two lanes, one block per CU: the other half of
+        // each CU stays free for the other lane's FFT blocks (k1_blocks_per_cu)
         const int grid = (int)std::min<long>(nitems, (long)k1_blocks_per_cu() * cus);
-        if (form == 8)                                    // per-pixel atomics always (experiment)
-            launch_form<512, true, 4, true, false, 0>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
-                                                      k255, out0, a_stride, h_stride, cshift2);
-        else
-            launch_form<512, true, 4, true, false, 2>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
-                                                      k255, out0, a_stride, h_stride, cshift2);
+        launch_form<512, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0, a_stride,
+                               h_stride, cshift2);
     } else {                                              // one 1024-thread block per CU
         const int grid = (int)std::min<long>(nitems, cus);
         // the triangular code table leaves 31 KiB more for lane copies of the
         // cells (fine grids: 36/4/5's 3312 hue cells only fit with it)
         const int cs_full = cshift_full(gp), cs_tri = cshift_tri1(gp);
         if (cs_tri < 0 && cs_full < 0) return hipErrorInvalidValue;   // k1t_cshift said no
-        // (form 9, experiment: the round-3 loop with the whole next chunk in registers)
         if (cs_tri > cs_full) {
             const size_t lds = (size_t)l_var(gp.tl, ncell, cs_tri, code_bytes<true>()).end;
-            if (form == 9)
-                launch_form<1024, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                        a_stride, h_stride, cs_tri);
-            else
-                launch_form<1024, true, 4, true, false, 2>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
-                                                           k255, out0, a_stride, h_stride, cs_tri);
+            launch_form<1024, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0, a_stride,
+                                    h_stride, cs_tri);
         } else {
             const size_t lds = (size_t)l_var(gp.tl, ncell, cs_full, code_bytes<false>()).end;
-            if (form == 9)
-                launch_form<1024, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                         a_stride, h_stride, cs_full);
-            else
-                launch_form<1024, false, 4, true, false, 2>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G,
-                                                            tabs, k255, out0, a_stride, h_stride, cs_full);
+            launch_form<1024, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
+                                     a_stride, h_stride, cs_full);
         }
     }
     return hipGetLastError();

@@ -47,8 +47,8 @@ struct K1Grid {
     int gs;          // gray_start: first gray / black group
     int ncell;       // HueCells::count; cell ncell is the dummy of deferred pixels
     int small_c;     // every c < 64: the boundary properties are bit masks
-    unsigned below_m[2];          // bit c (word c / 32): an exact boundary hue at B_c counts below it
-    unsigned defer_m[2];          // bit c: B_c is not a multiple of 60 (onb pixels defer)
+    unsigned long long below_m;   // bit c: an exact boundary hue at B_c counts below it
+    unsigned long long defer_m;   // bit c: B_c is not a multiple of 60 (onb pixels defer)
 };
 
 // a * b for 0 <= a, b < 2^24 (and a * b < 2^32): one full-rate v_mul_u32_u24
@@ -61,17 +61,16 @@ K1_HD int k1_mul(int a, int b) {
 #endif
 }
 
-// The reciprocals a pixel needs, per k in [1, 255] (k1_inv_init; LDS in the
-// kernel): 1 / k rounded to double (h = 60 X / kd and s = kd / kmax as one
-// multiply each, within an ulp of the exact rational) and to float (the
-// half-bin cell's fp32 quotient).  One 16-byte entry, one LDS read.
+// The reciprocals a pixel needs, per k in [1, 255]: 1 / k to double (h = 60 X
+// / kd and s = kd / kmax as one multiply each, within an ulp of the exact
+// rational) and to float (the half-bin cell's fp32 quotient).
 struct K1Inv {
     double inv;
     float rcp;
     unsigned pad;
 };
-// The same entry from the VALU: the fp32 reciprocal and one fp64 Newton step
-// (1 - k r is exact in an fma; ~2^-45 relative), no table read.
+// From the VALU: the fp32 reciprocal and one fp64 Newton step (1 - k r is
+// exact in an fma; ~2^-45 relative), no table read.
 K1_HD K1Inv k1_inv_valu(int k) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const float r = __builtin_amdgcn_rcpf((float)k);
@@ -81,10 +80,6 @@ K1_HD K1Inv k1_inv_valu(int k) {
     const double d = (double)r;
     const double e = std::fma(-(double)k, d, 1.0);
     return K1Inv{std::fma(d, e, d), r, 0u};
-}
-inline void k1_inv_init(K1Inv* t) {
-    t[0] = K1Inv{0.0, 0.0f, 0u};
-    for (int k = 1; k < 256; k++) t[k] = K1Inv{1.0 / (double)k, 1.0f / (float)k, 0u};
 }
 
 K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
@@ -99,13 +94,13 @@ K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
     G.ncell = 4 * G.gs + (g.ng + 1) * 2 * g.hp;
     // c < 720 / Lh (X < 6 kd)
     G.small_c = (720 + G.lh - 1) / G.lh <= 64;
-    G.below_m[0] = G.below_m[1] = G.defer_m[0] = G.defer_m[1] = 0u;
+    G.below_m = G.defer_m = 0ull;
     for (int c = 0; c < 64 && G.small_c; c++) {
         const bool mult60 = (c * G.lh) % 120 == 0;            // B_c = c Lh / 2 is a multiple of 60
         const int ch = c - g.hp;
         const bool below = mult60 && ch >= 0 && ((ch & 1) || ch == 0);
-        if (below) G.below_m[c >> 5] |= 1u << (c & 31);
-        if (!mult60) G.defer_m[c >> 5] |= 1u << (c & 31);
+        if (below) G.below_m |= 1ull << c;
+        if (!mult60) G.defer_m |= 1ull << c;
     }
 }
 
@@ -149,10 +144,11 @@ K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, 
     const bool onb = k1_mul(c, D) == n2;
     bool below, def;
     if (SMALL) {
-        // 32-bit words (a 64-bit shift and compare cost several VALU slots)
-        const bool hi = c >= 32;
-        below = onb && (((hi ? G.below_m[1] : G.below_m[0]) >> (c & 31)) & 1u);
-        def = onb && (((hi ? G.defer_m[1] : G.defer_m[0]) >> (c & 31)) & 1u);
+        // one 64-bit shift of a uniform mask per property (v_lshrrev_b64; the
+        // two 32-bit words selected by c >= 32 cost a compare, two moves of
+        // the words and a select each)
+        below = onb && (unsigned)(G.below_m >> c) & 1u;
+        def = onb && (unsigned)(G.defer_m >> c) & 1u;
     } else {
         const bool special = (kr == kg) | (kg == kb) | (kr == kb);
         const int ch = c - G.hp;

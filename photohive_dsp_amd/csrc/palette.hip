@@ -1488,11 +1488,11 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
     const long nitems = (long)n * nchunks;
     if (sums && (!hist || !fused_palette_ok(gp))) return hipErrorInvalidValue;
     // the fused palette pass over word-aligned images: the table K1 (k1.hip)
-    if (sums && aligned && fc.k1t_cshift >= 0 && !phd_knob("PHD_K1_OLD"))
+    if (sums && aligned && fc.k1t_cshift >= 0)
         return launch_k1t_batch(d_imgs, n, height, width, gp, tabs, out0, a_stride, h_stride, nchunks, k255,
                                 fc.k1t_cshift, fc.k1t_cshift2, st);
     // the statistics-only pass over word-aligned images: the lean kernel (stats.hip)
-    if (!hist && aligned && !phd_knob("PHD_STATS_K1"))
+    if (!hist && aligned)
         return launch_rgb_stats_batch(d_imgs, n, height, width, out0, a_stride, nchunks, st);
     const size_t lds = hsv_stats_lds(gp, hist, sums);
     const int cshift = sums ? k1_fused_cshift(gp) : k1_cshift(gp.tl);
@@ -1505,16 +1505,13 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
         kfn = fc.use_thr ? (aligned ? PHD_K1_FN(true, false, true, true) : PHD_K1_FN(true, false, false, true))
                          : (aligned ? PHD_K1_FN(true, false, true, false) : PHD_K1_FN(true, false, false, false));
     else
-        kfn = aligned ? PHD_K1_FN(false, false, true, true) : PHD_K1_FN(false, false, false, true);
+        kfn = PHD_K1_FN(false, false, false, true);       // (unaligned: aligned images took k_rgb_stats)
 #undef PHD_K1_FN
     // persistent blocks: as many as are resident at once
     (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kPalThreads, lds) != hipSuccess || per_cu < 1)
         per_cu = 1;
-    // blocks per CU (PHD_K1_PER_CU caps it, for co-residency experiments with the row FFT)
-    static const int cap = phd_knob("PHD_K1_PER_CU") ? atoi(phd_knob("PHD_K1_PER_CU")) : 0;
-    if (cap > 0 && per_cu > cap) per_cu = cap;
     const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
     void* args[] = {(void*)&d_imgs, (void*)&npix, (void*)&nchunks, (void*)&nitems, (void*)&gp, (void*)&fc,
                     (void*)&tabs, (void*)&k255, (void*)&out0, (void*)&a_stride, (void*)&h_stride,
@@ -1655,8 +1652,7 @@ hipError_t launch_partial_sums_batch(const uint8_t* const* d_imgs, const uint8_t
     const long npix = (long)height * width;
     bool aligned = true;
     for (int i = 0; i < n; i++) aligned = aligned && (reinterpret_cast<uintptr_t>(h_imgs[i]) & 3) == 0;
-    static const bool per_group = phd_knob("PHD_PARTIAL_PER_GROUP") != nullptr;
-    if (!per_group && max_per_image <= kPartImgMax && max_per_image > 1) {
+    if (max_per_image <= kPartImgMax && max_per_image > 1) {
         const size_t lds = PartImgLds::bytes(gp.tl);
         // (grid.y 16: same step time; 4: 4 % slower, the walks then outlast the FFTs they share the CUs with)
         // split each image's walk over ~4096 blocks in all, at least 64 per

@@ -162,6 +162,12 @@ thread_local int t_call_lanes = 1;
 CallLanes::CallLanes(int n) : prev_(t_call_lanes) { t_call_lanes = n; }
 CallLanes::~CallLanes() { t_call_lanes = prev_; }
 
+int fft_blocks_per_cu() {
+    // PHD_FFT_BPC (ablate build): persistent FFT blocks per CU on a split call
+    static const int env = phd_knob("PHD_FFT_BPC") ? atoi(phd_knob("PHD_FFT_BPC")) : 0;
+    return t_call_lanes >= 2 ? env : 0;
+}
+
 int k1_blocks_per_cu() {
     static const int env = phd_knob("PHD_K1_BPC") ? std::max(1, std::min(2, atoi(phd_knob("PHD_K1_BPC")))) : 0;
     // one block per CU only when this call is split over two lanes: the other
@@ -293,7 +299,7 @@ const FftPlanHost* get_plan(Context* c, int n, bool composite) {
 }
 
 const double2* get_ct_twiddles(Context* c, int n, bool rows) {
-    const auto key = std::make_pair(n, (rows ? 1 : 0) + 2 * ct_variant(rows));
+    const auto key = std::make_pair(n, rows ? 1 : 0);
     auto it = c->ct_tw.find(key);
     if (it != c->ct_tw.end()) return it->second;
     std::vector<int> rad;
@@ -331,7 +337,7 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
     *s = FftSel{};
     static const bool force_generic = phd_knob("PHD_FFT_GENERIC") != nullptr;   // A/B experiments only
     bool ct = !force_generic && ct_rows_plan(width, nullptr) && ct_cols_plan(height, nullptr) &&
-              fft_cols_ct_lds(height, nbins) <= 160 * 1024;
+              fft_cols_ct_lds(height) <= 160 * 1024;
     for (int i = 0; ct && i < n; i++)
         if (reinterpret_cast<uintptr_t>(imgs[i]) & 3) ct = false;   // dword row loads
     // the column pass sums bins from per-column run lists (ColRuns); a table
@@ -362,7 +368,7 @@ bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* con
         s->tw_c = get_ct_twiddles(c, height, false);
         if (!s->tw_r || !s->tw_c) return false;
         s->cbins = ColBins{runs ? runs->d_runs : nullptr, runs ? runs->d_seg : nullptr, runs ? runs->stride : 0};
-        s->col_blocks = fft_cols_ct_blocks(height, width / 2 + 1, nbins);
+        s->col_blocks = fft_cols_ct_blocks(height);
         return true;
     }
     if (!gfft_direct_ok(width) || !gfft_direct_ok(height)) return select_generic(c, height, width, nbins, s);

@@ -164,6 +164,9 @@ int num_cus();         // compute units of the current device
 // blocks: 7.89k against 7.66k images/s with two lanes, and 6.78k against
 // 7.07k with one, where K1 runs alone; PHD_K1_BPC overrides)
 int k1_blocks_per_cu();
+// Persistent blocks per CU of the compile-time FFT passes on this call (0:
+// as many as are resident)
+int fft_blocks_per_cu();
 // Scope guard: the calling thread's current call runs on n lanes (on_lanes)
 struct CallLanes {
     explicit CallLanes(int n);
@@ -269,87 +272,45 @@ hipError_t launch_fft_cols(const double2* inter, int height, int wf, const FftPl
 int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* lds, int* lds_bins);
 
 // ---- compile-time FFT plans (fft_ct.hip / fft_engine.h) ------------------------
-// X(length, variant, threads per block, radices...).  Variant 0 is production;
-// PHD_CT_ROWS_VARIANT / PHD_CT_COLS_VARIANT select another for tuning runs.
-// The first radix is odd (LDS bank-conflict-free first pass, fft_engine.h).
-// Rows need length % 4 == 0.
-// rows: X(length, variant, threads, radices...).  Measured at 4000x3000:
-// v0 43.2 us, v1 43.7, v2 47.3 (25 16 10 at 400 threads), v3 47.3, v4 56.0.
-// A last pass that pairs butterflies b and NB - b and separates the two rows'
-// spectra in registers (no LDS write of the last pass, no split reads) was
-// correct (1e-15) but slower: 48.9 us at 256 threads (5 8 10 10), 49.5 at
-// 512 (5 10 20 4, spills), 59.6 / 64.6 at 512 / 384 threads (5 8 10 10).
-#define PHD_CT_ROWS(X)              \
-    X(4000, 0, 512, 5, 8, 10, 10)   \
-    X(4000, 1, 256, 25, 16, 10)     \
-    X(4000, 2, 400, 25, 16, 10)     \
-    X(4000, 3, 256, 5, 8, 10, 10)   \
-    X(4000, 4, 384, 5, 8, 10, 10)   \
-    X(6000, 0, 512, 6, 10, 10, 10)  \
-    X(6000, 1, 768, 6, 10, 10, 10)  \
-    X(3000, 0, 384, 5, 6, 10, 10)   \
-    X(2000, 0, 256, 5, 4, 10, 10)   \
+// X(length, threads per block, radices...).  The first radix is odd (LDS
+// bank-conflict-free first pass, fft_engine.h).  Rows need length % 4 == 0.
+// Plan choices measured in rounds 2-4 (DESIGN.md sections 9-11; the rejected
+// variants live in git history): rows of 4000 at 512 threads 43.2 us against
+// 43.7 for (25 16 10) at 256, 47.3 at 400, 56.0 at 384; a last row pass that
+// separates the two rows' spectra in registers 48.9-64.6.  Columns of 3000:
+// (15 10 20) at 256 threads 54.8 us (ct_sweep), (15 20 10) 55.5, (25 12 10)
+// 56.0, four-pass plans at 300 / 512 threads 61.2 / 61.4, two columns per
+// block 63.2, register prefetch of the next column 64.5-72.3, pass 0 from
+// registers 83.0, three blocks per CU at 168 VGPRs 94-107, global-atomic bins
+// 92-148.  Columns of 6000: (15 20 20) 128 us, (10 20 30) 133; of 4000 at 256
+// threads 130 us, 320 threads 126 (two blocks per CU since round 4's run
+// lists); rows of 6000 at 512 threads 93 us.
+#define PHD_CT_ROWS(X)           \
+    X(4000, 512, 5, 8, 10, 10)   \
+    X(6000, 512, 6, 10, 10, 10)  \
+    X(3000, 384, 5, 6, 10, 10)   \
+    X(2000, 256, 5, 4, 10, 10)   \
     /* config 5's sizes below 3 MP (round 3; batched launches, launch_fft_rows_ct_batch) */ \
-    X(2048, 0, 256, 8, 16, 16)      \
-    X(1920, 0, 256, 15, 8, 16)      \
-    X(1280, 0, 256, 5, 16, 16)      \
-    X(720, 0, 192, 5, 9, 16)        \
-    X(640, 0, 128, 5, 8, 16)        \
-    X(480, 0, 128, 5, 6, 16)        \
-    X(512, 0, 64, 8, 8, 8)
-// columns: X(length, variant, threads per column, flags, radices...); flags:
-// columns per block (1, 2) | 4 no register prefetch | 8 bins by global atomics.
-// Measured at 4000x3000 (tools/ct_sweep.py): v0 54.8 us, v2 55.5, v3 56.0,
-// v4 61.4, v5 61.2, v1 (2 columns, register prefetch, spills) 63.2; global
-// atomic bins 92-148 us (contention), so no variant uses them.
-// Config-5 lengths (tools/ct_sweep.py, 6000x4000 and 4000x6000): columns of
-// 6000 v0 128 us, (10 20 30) 133, 384 threads 143, 768 threads 173; columns
-// of 4000 at 320 threads 126 us, 256 threads 130, (16 25 10) 164, 384
-// threads 182; rows of 6000 at 512 / 768 threads 93 us, 384 threads 103.
-// Columns of 3000 at 320 threads 73 us, 192 threads 67 (v0: 53-58).
-// Round 3: columns of 4000 at 256 threads 143 us with the full bin table (one
-// block per CU by LDS), 104 us with per-block bin windows (two blocks per CU,
-// ColBins), against 159-162 us at 320 threads: 256 threads is variant 0.
-// Measured and removed in round 3: an LDS-DMA form
-// that streams the next column into LDS during the current column's last pass
-// (one column per block with bin windows: 55.9-58.6 against 54.9-56.8 us; two
-// columns per block in lockstep 75 us); plans of 3000 at 384 / 512 threads
-// (5 6 5 10 10, 15 20 10: 69.7-91 us).
-#define PHD_CT_COLS(X)                 \
-    X(3000, 0, 256, 5, 15, 10, 20)     \
-    X(3000, 1, 384, 2, 5, 6, 10, 10)   \
-    X(3000, 2, 256, 5, 15, 20, 10)     \
-    X(3000, 3, 256, 5, 25, 12, 10)     \
-    X(3000, 4, 512, 5, 5, 6, 10, 10)   \
-    X(3000, 5, 300, 5, 5, 6, 10, 10)   \
-    X(3000, 6, 256, 2, 15, 10, 20)     \
-    X(3000, 7, 256, 6, 15, 10, 20)     \
-    X(3000, 8, 192, 2, 15, 10, 20)     \
-    X(3000, 9, 256, 33, 15, 10, 20)    \
-    X(3000, 10, 256, 33, 15, 20, 10)   \
-    X(3000, 11, 256, 33, 25, 12, 10)   \
-    X(3000, 12, 256, 1, 15, 20, 10)    \
-    X(3000, 13, 256, 1, 15, 10, 20)    \
-    X(3000, 14, 256, 1, 10, 15, 20)    \
-    X(3000, 15, 256, 5, 10, 15, 20)    \
-    X(3000, 16, 256, 69, 15, 10, 20)   \
-    X(3000, 17, 256, 69, 15, 20, 10)   \
-    X(3000, 18, 256, 69, 10, 15, 20)   \
-    X(3000, 19, 256, 69, 25, 12, 10)   \
-    X(6000, 0, 512, 5, 15, 20, 20)     \
-    X(6000, 1, 512, 5, 10, 20, 30)     \
-    X(4000, 0, 256, 5, 10, 20, 20)     \
-    X(4000, 1, 320, 5, 10, 20, 20)     \
-    X(2000, 0, 256, 5, 10, 10, 20)     \
+    X(2048, 256, 8, 16, 16)      \
+    X(1920, 256, 15, 8, 16)      \
+    X(1280, 256, 5, 16, 16)      \
+    X(720, 192, 5, 9, 16)        \
+    X(640, 128, 5, 8, 16)        \
+    X(480, 128, 5, 6, 16)        \
+    X(512, 64, 8, 8, 8)
+#define PHD_CT_COLS(X)           \
+    X(3000, 256, 15, 10, 20)     \
+    X(6000, 512, 15, 20, 20)     \
+    X(4000, 256, 10, 20, 20)     \
+    X(2000, 256, 10, 10, 20)     \
     /* config 5's sizes below 3 MP (round 3; batched launches, launch_fft_cols_ct_batch) */ \
-    X(1536, 0, 256, 5, 3, 8, 8, 8)     \
-    X(1080, 0, 192, 5, 15, 8, 9)       \
-    X(1280, 0, 256, 5, 5, 16, 16)      \
-    X(720, 0, 192, 5, 5, 9, 16)        \
-    X(640, 0, 128, 5, 5, 8, 16)        \
-    X(480, 0, 128, 5, 5, 6, 16)        \
-    X(512, 0, 64, 5, 8, 8, 8)
-int ct_variant(bool rows);
+    X(1536, 256, 3, 8, 8, 8)     \
+    X(1080, 192, 15, 8, 9)       \
+    X(1280, 256, 5, 16, 16)      \
+    X(720, 192, 5, 9, 16)        \
+    X(640, 128, 5, 8, 16)        \
+    X(480, 128, 5, 6, 16)        \
+    X(512, 64, 8, 8, 8)
 // radices of the compile-time plan for a row / column length (false: none)
 bool ct_rows_plan(int w, std::vector<int>* radices);
 bool ct_cols_plan(int h, std::vector<int>* radices);
@@ -376,16 +337,16 @@ struct ColBins {
     const uint8_t* seg = nullptr;    // [wf][T] the run holding each thread's first row
     int rstride = 0;                 // entries per column
 };
-size_t fft_cols_ct_lds(int height, int nlb);
+size_t fft_cols_ct_lds(int height);
 // threads per column of the compile-time column plan for a height (0: none)
 int fft_cols_ct_threads(int height);
 // log_mant (phd_device.h) over n positive doubles (tests)
 hipError_t launch_log_mant(const double* x, double* y, long n, hipStream_t st);
-// persistent grid of the column kernel (= entries of fmax_part); nlb unused
-// since the bins are summed per run (round 4)
-int fft_cols_ct_blocks(int height, int wf, int nlb);
+// persistent grid of the column kernel (= entries of fmax_part)
+int fft_cols_ct_blocks(int height);
 // tw: the plan's per-pass tables W_{NS*R}^jm (jm < NS) for passes 1.. (host built).
 // The row pass transforms the luma as is (sums unused): it does not wait for K1.
+// rsum (optional, the blur-only path): the image's exact channel sums, accumulated
 hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const unsigned long long* sums,
                               const double* k255, const double2* tw, double2* inter, hipStream_t st,
                               unsigned long long* rsum = nullptr);

@@ -36,7 +36,7 @@ size_t al(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
 struct Layout {
     // per-image records
     size_t a_sums, a_hist, a_spart, a_gsum, a_gcell, a_bytes;  // read back after K1 (zeroed)
-    size_t c_bins, c_fmax, c_pal, c_sharp, c_rsum, c_bytes; // read back at the end (zeroed)
+    size_t c_bins, c_fmax, c_pal, c_sharp, c_bytes;         // read back at the end (zeroed)
     size_t b_rules, b_search, b_off, b_bytes;               // uploaded before K3
     size_t chunk_bytes;                                      // device only
     size_t ptr_bytes;                                        // image pointer array (pinned -> device)
@@ -67,8 +67,7 @@ Layout make_layout(int n, int tl, int nchunks, int nbins, int ncrops, int ncolbl
     L.c_fmax = al(sizeof(double) * nbins);
     L.c_pal = L.c_fmax + al(sizeof(double) * (ncolblocks > 0 ? ncolblocks : 1));
     L.c_sharp = L.c_pal + al(sizeof(double) * 4 * tl);
-    L.c_rsum = L.c_sharp + al(sizeof(double) * 2 * (ncrops > 0 ? ncrops : 1));
-    L.c_bytes = L.c_rsum + al(3 * sizeof(unsigned long long));
+    L.c_bytes = L.c_sharp + al(sizeof(double) * 2 * (ncrops > 0 ? ncrops : 1));
     L.b_rules = 0;
     L.b_search = al(sizeof(GroupRule) * tl);
     L.b_off = L.b_search + al(sizeof(int) * tl);
@@ -1250,7 +1249,8 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
     const size_t r_bins = 0, r_fmax = al(sizeof(double) * nbins);
     const size_t r_sums = r_fmax + al(sizeof(double) * (fs.col_blocks > 0 ? fs.col_blocks : 1));
     const size_t r_spart = r_sums + al(6 * sizeof(unsigned long long));
-    const size_t rb = r_spart + al(sizeof(double) * nchunks);
+    const size_t r_kd = r_spart + al(sizeof(double) * nchunks);   // the statistics pass's sums of d (unused)
+    const size_t rb = r_kd + al(256 * sizeof(unsigned long long));
     const size_t ptrs = al(sizeof(void*) * (size_t)n_images);
     const size_t inter_one = sizeof(double2) * inter_elems(height, width);
     if (!ensure_device(&c->d_ws, &c->ws_bytes, (size_t)n_images * rb + ptrs) ||
@@ -1278,6 +1278,7 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
         PaletteDev pd{};
         pd.sums = (unsigned long long*)(dw + r_sums);
         pd.s_part = (double*)(dw + r_spart);
+        pd.kd_sum = (unsigned long long*)(dw + r_kd);
         if ((e = launch_hsv_stats_batch((const uint8_t* const*)(dw + (size_t)n_images * rb), n_images, height,
                                         width, gp, cls->fc, cls->d, pd, (long)rb, 0, nchunks, c->d_k255, false,
                                         false, all_aligned(hptr, n_images), st)) != hipSuccess)
@@ -1625,13 +1626,16 @@ extern "C" int phd_debug_time_kernel(int kernel, const uint8_t* d_rgb, int heigh
     pd.s_part = (double*)(dw + 256 + 4 * 4096);
     pd.chunk_hist = (unsigned short*)(dw + 256 + 4 * 4096 + 8 * (size_t)nchunks);
     // K1 is timed as the report runs it: fused when the report fuses
-    const bool fused = ds <= 1 && phd_knob("PHD_PALETTE_TWO_PASS") == nullptr && fused_palette_ok(gp);
+    const bool fused = ds <= 1 && fused_palette_ok(gp);
     void* fscratch = nullptr;
-    if (fused) {
-        if (hipMalloc(&fscratch, sizeof(double) * 3 * gp.tl + sizeof(unsigned) * HueCells::count(gp)) != hipSuccess)
+    if (fused || kernel == kNumKernels) {
+        // the fused K1's group sums and cell counts; the statistics pass's sums of d
+        if (hipMalloc(&fscratch, sizeof(double) * 3 * gp.tl + sizeof(unsigned) * HueCells::count(gp) +
+                                     256 * sizeof(unsigned long long)) != hipSuccess)
             return -1;
-        pd.gsum = (double*)fscratch;
-        pd.gcell = (unsigned*)((double*)fscratch + 3 * gp.tl);
+        pd.kd_sum = (unsigned long long*)fscratch;
+        pd.gsum = (double*)fscratch + 256;
+        pd.gcell = (unsigned*)((double*)fscratch + 256 + 3 * gp.tl);
     }
     struct FreeOnExit {
         void* p;

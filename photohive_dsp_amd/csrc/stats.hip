@@ -8,21 +8,17 @@
 // 408-414).  No group histogram: this is the HBM-streaming pass, sized so the
 // VALU work per byte stays below the HBM rate.
 //
-// Per thread, 4 pixels = 12 bytes = one dwordx3 load (a wave reads 768
-// contiguous bytes).  The 12 bytes are regrouped by v_perm into six u16 pairs
-// (R02 = {r0, r2}, R13 = {r1, r3}, likewise G and B); then per 4 pixels:
+// Per thread, 4 pixels = 12 bytes = one non-temporal dwordx3 load (a wave
+// reads 768 contiguous bytes, streamed once: 0.74 of the HBM peak against
+// 0.70-0.72 with plain loads).  The 12 bytes are regrouped by v_perm into six
+// u16 pairs (R02 = {r0, r2}, R13 = {r1, r3}, likewise G and B); then per 4
+// pixels:
 //   * moments: v_dot2_u32_u16 of each pair with {1, 1} and with itself (exact
 //     u32 per thread, flushed to u64 per run);
-//   * max / min: v_pk_max_u16 / v_pk_min_u16, d = max - min (v_pk_sub);
-//   * s for a pixel pair (a, b): s_a + s_b = (d_a M_b + d_b M_a) / (M_a M_b),
-//     numerator and denominator each one v_dot2 (2 M_a M_b = dot2(M, swap M)),
-//     one fp32 reciprocal per pair, summed in fp32 per item and in fp64 per run.
-//     M is raised to 1 for black pixels (d = 0).
+//   * max / min: v_pk_max_u16 / v_pk_min_u16, d = max - min (v_pk_sub).
 // rgb2hsv's s is d / max except 0.999999 for d == max (min == 0 < max,
-// src/image_processing.c:408-414).
-//
-// Default, PHD_STATS_MODE=3 (the reference's width): s is never divided per
-// pixel.  sum(s) = sum_m (sum of d over the pixels with max = m) / m
+// src/image_processing.c:408-414), and it is never divided per pixel
+// (the reference's width).  sum(s) = sum_m (sum of d over the pixels with max = m) / m
 //                  - (1 - 0.999999) * #(min == 0 < max)
 // (a d == max pixel adds m / m = 1 to the first term; 1 - 0.999999 is exact in
 // fp64), so the pass only needs, per image, the exact integer sum of d per max
@@ -30,17 +26,9 @@
 // histogram (32 copies, padded to 257 so lanes fall on distinct banks), folded
 // into the image's u64 buckets when a run ends; the host finishes the sum in
 // fp64 (phd_hsv_stats_batch_device).  Within ~1e-15 of the reference's
-// sequential fp64 sum of the per-pixel doubles.
-//
-// The earlier fp32 forms (kept for measurement):
-//   PHD_STATS_MODE=0: fp32 pair sums, d == max pixels add 1: S-bar high by
-//                     <= 1e-6 relative; 0.71-0.74 of the HBM peak (round 2);
-//   PHD_STATS_MODE=1: + a count of min == 0 < max pixels (packed u16), each
-//                     taking (1 - 0.999999) off at the flush: ~1e-7 relative,
-//                     0.60-0.63;
-//   PHD_STATS_MODE=2: + compensated fp32 quotients and Kahan sums: ~2e-9, 0.57;
-//   (an fp64 v_rcp_f64 + Newton form: 0.54, not kept).
-// The full report's K1 (k1.hip) keeps the exact fp64 s.
+// sequential fp64 sum of the per-pixel doubles.  (Rounds 2-3 measured fp32
+// pair-quotient forms at 0.57-0.74 of the peak and 1e-6 to 2e-9 relative; git
+// history.)  The full report's K1 (k1.hip) keeps the exact fp64 s.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -57,25 +45,19 @@ constexpr int kStGroups = kChunk / (4 * kStThreads);
 static_assert(kStGroups == 8, "stats tile");
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) unsigned gu32s;
 
 __device__ __forceinline__ u16x2 as_u16x2(unsigned x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ unsigned as_u32(u16x2 x) { return __builtin_bit_cast(unsigned, x); }
 
 struct StatAcc {
     unsigned sr, sg, sb, qr, qg, qb;         // per-thread moments of the run (u32: <= 1024 items)
-    f32x2 s;                                 // sum(s_a + s_b) / 2 of the item's pixel pairs
-    f32x2 c;                                 // kMode 2: minus its Kahan compensation (and the residuals)
-    double s64;                              // kMode >= 1: the partial final group's s (fp64)
+    double s64;                              // the partial final group's s (fp64)
     u16x2 n1;                                // pixels with min == 0 < max (<= 8 per item per half)
 };
 
-// 4 pixels (3 little-endian words w0..w2 = r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3).
-// kMode 0: plain fp32 pair sums (round 1); 1: + the 0.999999 rule; 2: +
-// compensated quotients and Kahan sums; 3 (default): d added to bucket max of
-// this lane's LDS histogram copy `hk` + the 0.999999 count
-template <int kMode>
+// 4 pixels (3 little-endian words w0..w2 = r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3):
+// moments, d added to bucket max of this lane's LDS histogram copy `hk`, the
+// 0.999999 count
 __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, StatAcc& a, unsigned* hk) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as_u16x2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
@@ -101,47 +83,13 @@ __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, Sta
     const u16x2 n02 = __builtin_elementwise_min(__builtin_elementwise_min(r02, g02), b02);
     const u16x2 n13 = __builtin_elementwise_min(__builtin_elementwise_min(r13, g13), b13);
     const u16x2 d02 = m02 - n02, d13 = m13 - n13;
-    if constexpr (kMode == 3) {
-        atomicAdd(&hk[m02.x], (unsigned)d02.x);
-        atomicAdd(&hk[m13.x], (unsigned)d13.x);
-        atomicAdd(&hk[m02.y], (unsigned)d02.y);
-        atomicAdd(&hk[m13.y], (unsigned)d13.y);
-        const u16x2 zero = {0, 0};
-        a.n1 += (u16x2)((n02 == zero) & (m02 != zero)) & one;
-        a.n1 += (u16x2)((n13 == zero) & (m13 != zero)) & one;
-        return;
-    }
-    const u16x2 M02 = __builtin_elementwise_max(m02, one), M13 = __builtin_elementwise_max(m13, one);
-    const u16x2 S02 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M02), as_u32(M02), 16));
-    const u16x2 S13 = as_u16x2(__builtin_amdgcn_alignbit(as_u32(M13), as_u32(M13), 16));
-    // (d_a M_b + d_b M_a) and 2 M_a M_b, exact integers < 2^18
-    const unsigned nu02 = __builtin_amdgcn_udot2(d02, S02, 0u, false), nu13 = __builtin_amdgcn_udot2(d13, S13, 0u, false);
-    const unsigned de02 = __builtin_amdgcn_udot2(M02, S02, 0u, false), de13 = __builtin_amdgcn_udot2(M13, S13, 0u, false);
-    if constexpr (kMode < 2) {
-        const f32x2 num = {(float)nu02, (float)nu13};
-        const f32x2 den = {(float)de02, (float)de13};
-        const f32x2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-        a.s = __builtin_elementwise_fma(num, rc, a.s);
-    } else {
-        // (s_a + s_b) / 2 = num / den as q + q2 (q = num rcp(den), q2 = the exact
-        // fp32 residual fma(-q, den, num) times rcp(den): ~2^-46 relative), both
-        // added with Kahan compensation; two pairs per packed instruction
-        const f32x2 num = {(float)nu02, (float)nu13};
-        const f32x2 den = {(float)de02, (float)de13};
-        const f32x2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-        const f32x2 q = num * rc;
-        const f32x2 q2 = __builtin_elementwise_fma(-q, den, num) * rc;
-        const f32x2 y = q - a.c;                      // Kahan: a.s + a.c carries the sum
-        const f32x2 t = a.s + y;
-        a.c = (t - a.s) - y - q2;
-        a.s = t;
-    }
-    if constexpr (kMode >= 1) {
-        // min == 0 < max: rgb2hsv's 0.999999 instead of d / max = 1
-        const u16x2 zero = {0, 0};
-        a.n1 += (u16x2)((n02 == zero) & (m02 != zero)) & one;
-        a.n1 += (u16x2)((n13 == zero) & (m13 != zero)) & one;
-    }
+    atomicAdd(&hk[m02.x], (unsigned)d02.x);
+    atomicAdd(&hk[m13.x], (unsigned)d13.x);
+    atomicAdd(&hk[m02.y], (unsigned)d02.y);
+    atomicAdd(&hk[m13.y], (unsigned)d13.y);
+    const u16x2 zero = {0, 0};
+    a.n1 += (u16x2)((n02 == zero) & (m02 != zero)) & one;
+    a.n1 += (u16x2)((n13 == zero) & (m13 != zero)) & one;
 }
 
 // One launch over a batch of same-size, 4-byte-aligned images.  Work items
@@ -152,26 +100,22 @@ __device__ __forceinline__ void stat4(unsigned w0, unsigned w1, unsigned w2, Sta
 // atomics) and out.s_part[first chunk of the run] (one fp64 per run).
 constexpr int kHistCopies = 32, kHistPad = 257;
 
-template <bool kNT, int kMode>
 __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* const* __restrict__ imgs, long npix,
                                                               int nchunks, long nitems, PaletteDev out,
                                                               long a_stride) {
     __shared__ unsigned long long red[kStThreads / 64][8];
-    // kMode 3: sum of d per max value, one copy per lane of a half-wave
-    __shared__ unsigned hist[kMode == 3 ? kHistCopies * kHistPad : 1];
+    // sum of d per max value, one copy per lane of a half-wave
+    __shared__ unsigned hist[kHistCopies * kHistPad];
     const int tid = threadIdx.x;
-    unsigned* hk = hist + (kMode == 3 ? (tid & (kHistCopies - 1)) * kHistPad : 0);
-    if constexpr (kMode == 3) {
-        for (int i = tid; i < kHistCopies * kHistPad; i += kStThreads) hist[i] = 0u;
-        __syncthreads();
-    }
+    unsigned* hk = hist + (tid & (kHistCopies - 1)) * kHistPad;
+    for (int i = tid; i < kHistCopies * kHistPad; i += kStThreads) hist[i] = 0u;
+    __syncthreads();
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                 // block-uniform
     const long full_end = npix & ~3L;                       // groups wholly inside the image
     int img = (int)(it0 / nchunks), c = (int)(it0 - (long)img * nchunks);
     const uint8_t* ip = imgs[img];
-    StatAcc a{0, 0, 0, 0, 0, 0, {0.f, 0.f}, {0.f, 0.f}, 0.0, {0, 0}};
-    double ssum = 0.0;
+    StatAcc a{0, 0, 0, 0, 0, 0, 0.0, {0, 0}};
     int seg_c0 = c;
     long seg_it0 = it0;
     for (long it = it0; it < it1; it++) {
@@ -184,42 +128,29 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
 #pragma unroll
             for (int st = 0; st < kStGroups; st++) {
                 gu32s* q = (gu32s*)(ip + (off0 + 12u * kStThreads * st));
-                if constexpr (kNT) {                       // streamed once: non-temporal
-                    w[st][0] = __builtin_nontemporal_load(q);
-                    w[st][1] = __builtin_nontemporal_load(q + 1);
-                    w[st][2] = __builtin_nontemporal_load(q + 2);
-                } else {
-                    w[st][0] = q[0];
-                    w[st][1] = q[1];
-                    w[st][2] = q[2];
-                }
+                w[st][0] = __builtin_nontemporal_load(q);          // streamed once
+                w[st][1] = __builtin_nontemporal_load(q + 1);
+                w[st][2] = __builtin_nontemporal_load(q + 2);
             }
 #pragma unroll
-            for (int st = 0; st < kStGroups; st++) stat4<kMode>(w[st][0], w[st][1], w[st][2], a, hk);
+            for (int st = 0; st < kStGroups; st++) stat4(w[st][0], w[st][1], w[st][2], a, hk);
         } else {
 #pragma unroll 1
             for (int st = 0; st < kStGroups; st++) {
                 const long p0 = base + 4L * tid + 4L * kStThreads * st;
                 if (p0 < full_end) {
                     gu32s* q = (gu32s*)(ip + 3 * p0);
-                    stat4<kMode>(q[0], q[1], q[2], a, hk);
+                    stat4(q[0], q[1], q[2], a, hk);
                 }
             }
         }
-        // the item's pair sums (a factor 1/2) into fp64
-        ssum += (double)a.s.x + (double)a.s.y;
-        if constexpr (kMode == 2) ssum -= (double)a.c.x + (double)a.c.y;
-        a.s = f32x2{0.f, 0.f};
-        a.c = f32x2{0.f, 0.f};
         if (tid == 0 && base + kChunk >= npix) {
             // the < 4 pixels of a partial final group: exact fp64 s
             for (long p = full_end; p < npix; p++) {
                 const int kr = ip[3 * p], kg = ip[3 * p + 1], kb = ip[3 * p + 2];
                 a.sr += kr; a.sg += kg; a.sb += kb;
                 a.qr += kr * kr; a.qg += kg * kg; a.qb += kb * kb;
-                // the pair sums carry a factor 1/2; fp64 s (0.999999 included)
-                if constexpr (kMode == 0) ssum += 0.5 * sat_only(kr, kg, kb);
-                else a.s64 += sat_only(kr, kg, kb);
+                a.s64 += sat_only(kr, kg, kb);                   // fp64 s (0.999999 included)
             }
         }
         const int cimg = img;
@@ -235,12 +166,9 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
             unsigned long long m64[6];
 #pragma unroll
             for (int k = 0; k < 6; k++) m64[k] = wave_sum((unsigned long long)mom[k]);
-            double mine = 2.0 * ssum;                 // sum of s
-            if constexpr (kMode >= 1) {
-                // less (1 - 0.999999) per min == 0 < max pixel; the partial group's exact s
-                const unsigned n1 = (unsigned)a.n1.x + (unsigned)a.n1.y;
-                mine = __builtin_fma(-(1.0 - 0.999999), (double)n1, mine + a.s64);
-            }
+            // less (1 - 0.999999) per min == 0 < max pixel; the partial group's exact s
+            const unsigned n1 = (unsigned)a.n1.x + (unsigned)a.n1.y;
+            const double mine = __builtin_fma(-(1.0 - 0.999999), (double)n1, a.s64);
             const double sw = wave_sum(mine);
             if (lane_id() == 0) {
 #pragma unroll
@@ -248,7 +176,7 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
                 reinterpret_cast<double*>(red[wv])[6] = sw;
             }
             __syncthreads();
-            if constexpr (kMode == 3) {
+            {
                 // the run's buckets into the image's (exact u64 sums, any order)
                 if (tid < 256) {
                     unsigned long long b = 0;
@@ -274,8 +202,7 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
                 // one slot per run (distinct first chunks)
                 reinterpret_cast<double*>(reinterpret_cast<char*>(out.s_part) + cimg * a_stride)[seg_c0] = t;
             }
-            a = StatAcc{0, 0, 0, 0, 0, 0, {0.f, 0.f}, {0.f, 0.f}, 0.0, {0, 0}};
-            ssum = 0.0;
+            a = StatAcc{0, 0, 0, 0, 0, 0, 0.0, {0, 0}};
             seg_c0 = c;
             seg_it0 = it + 1;
             __syncthreads();                                  // red is reused by the next flush
@@ -289,39 +216,15 @@ hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
                                   long a_stride, int nchunks, hipStream_t st) {
     const long npix = (long)height * width;
     const long nitems = (long)n * nchunks;
-    // non-temporal loads (the pixels are streamed once): 0.74 of the HBM peak
-    // against 0.70-0.72 with plain loads (PHD_STATS_PLAIN=1)
-    static const bool nt = phd_knob("PHD_STATS_PLAIN") == nullptr;
-    // PHD_STATS_MODE (config 3, 512 x 1080p, fraction of the 8 TB/s peak):
-    // 3 (default) exact sum of d per max value; 0 fp32 pair sums 0.71-0.74 (round
-    // 2); 1 + the 0.999999 count 0.60-0.63; 2 + compensated quotients 0.57
-    static const int mode = phd_knob("PHD_STATS_MODE") ? atoi(phd_knob("PHD_STATS_MODE")) : 3;
-#define PHD_ST(NT, M)                                                                                          \
-    do {                                                                                                       \
-        /* the persistent grid is sized for the variant launched */                                            \
-        static const int per_cu_ = [] {                                                                        \
-            int b = 0;                                                                                         \
-            return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, (const void*)k_rgb_stats<NT, M>,           \
-                                                                kStThreads, 0) == hipSuccess && b > 0 ? b : 1; \
-        }();                                                                                                   \
-        const int grid = (int)std::min<long>(nitems, (long)per_cu_ * num_cus());                               \
-        phd_launch((k_rgb_stats<NT, M>), dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems,   \
-                   out0, a_stride);                                                                            \
-    } while (0)
-    if (mode == 3 && out0.kd_sum) {
-        if (nt) PHD_ST(true, 3);
-        else PHD_ST(false, 3);
-    } else if (mode == 0) {
-        if (nt) PHD_ST(true, 0);
-        else PHD_ST(false, 0);
-    } else if (mode == 2) {
-        if (nt) PHD_ST(true, 2);
-        else PHD_ST(false, 2);
-    } else {
-        if (nt) PHD_ST(true, 1);
-        else PHD_ST(false, 1);
-    }
-#undef PHD_ST
+    if (!out0.kd_sum) return hipErrorInvalidValue;       // the sums of d per max value are the pass's s
+    // the persistent grid: as many blocks as are resident at once
+    static const int per_cu = [] {
+        int b = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, (const void*)k_rgb_stats, kStThreads, 0) ==
+                       hipSuccess && b > 0 ? b : 1;
+    }();
+    const int grid = (int)std::min<long>(nitems, (long)per_cu * num_cus());
+    phd_launch(k_rgb_stats, dim3(grid), dim3(kStThreads), 0, st, d_imgs, npix, nchunks, nitems, out0, a_stride);
     return hipGetLastError();
 }
 

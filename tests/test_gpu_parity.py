@@ -201,22 +201,18 @@ def test_hsv_stats_batch_config3_shape():
     np.testing.assert_allclose(sat[0], orc.palette(img)["average_saturation"], rtol=STATS_SAT_RTOL)
 
 
-# The statistics-only pass (stats.hip).  Default (PHD_STATS_MODE=3): exact
-# integer sums of d per max value, finished on the host in fp64 -- the
-# reference's width, within 1e-12 of its sequential fp64 sum.  The fp32 forms
-# kept for measurement: 0 (d == max adds 1, fp32 pair sums) within 2e-6, 1 / 2
-# within 3e-7 / 5e-9 (north_star allows 1e-4 for float fields).  The moments are
-# exact in every mode.
-STATS_MODE = int(os.environ.get("PHD_STATS_MODE", "3"))
-STATS_SAT_RTOL = {0: 2e-6, 1: 3e-7, 2: 5e-9, 3: 1e-12}[STATS_MODE]
+# The statistics-only pass (stats.hip): exact integer sums of d per max value,
+# finished on the host in fp64 -- the reference's width, within 1e-12 of its
+# sequential fp64 sum.  The moments are exact.
+STATS_SAT_RTOL = 1e-12
 
 
 def stats_sat_rtol(npix):
-    """The exact mode is bounded by the reference's own rounding: its S-bar is a
+    """The pass is bounded by the reference's own rounding: its S-bar is a
     sequential fp64 sum of npix per-pixel doubles (src/image_processing.c:533-540),
     whose error bound is npix * 2^-53 relative (reached on images where every
     pixel adds the same 0.999999)."""
-    return max(STATS_SAT_RTOL, npix * 2.0 ** -53) if STATS_MODE == 3 else STATS_SAT_RTOL
+    return max(STATS_SAT_RTOL, npix * 2.0 ** -53)
 
 
 @pytest.mark.parametrize("kind,h,w", [("uniform", 401, 577), ("black", 400, 400), ("saturated", 360, 1200),
@@ -271,7 +267,7 @@ def test_hsv_stats_pass_batch_512_1080p_consistency():
         s1, a1 = hsv_stats_device(v[i:i + 1])
         assert [getattr(stats[i], f) for f in ("Br", "Bg", "Bb", "Cr", "Cg", "Cb")] == \
             [getattr(s1[0], f) for f in ("Br", "Bg", "Bb", "Cr", "Cg", "Cb")]
-        np.testing.assert_allclose(sat[i], a1[0], rtol=1e-14 if STATS_MODE == 3 else 1e-9)
+        np.testing.assert_allclose(sat[i], a1[0], rtol=1e-14)
     img = synth.uniform(h, w, 511)
     np.testing.assert_allclose(sat[511], orc.palette(img)["average_saturation"], rtol=STATS_SAT_RTOL)
     del t, v

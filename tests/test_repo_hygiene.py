@@ -23,3 +23,30 @@ def test_production_library_reads_few_environment_switches():
     knob = src[src.index("inline const char* phd_knob"):]
     knob = knob[:knob.index("\n}\n")]
     assert "#ifdef PHD_ABLATE_BUILD" in knob and "return nullptr;" in knob
+
+
+def test_production_library_holds_only_launched_kernel_forms():
+    """Measured-and-rejected kernel variants are not compiled into the
+    production .so (round 5): one compile-time row / column kernel per plan
+    of PHD_CT_ROWS / PHD_CT_COLS, K1's two-block and one-block forms only (x
+    the small-grid mask form), one statistics kernel."""
+    import subprocess
+    so = os.path.join(ROOT, "photohive_dsp_amd", "PhotoHive_DSP_lib", "libreport_data.so")
+    out = subprocess.run(["nm", "-C", so], capture_output=True, text=True, check=True).stdout
+    stubs = re.findall(r"__device_stub__(\w+)", out)
+    count = {k: stubs.count(k) for k in set(stubs)}
+    with open(os.path.join(ROOT, "photohive_dsp_amd", "csrc", "phd_internal.h")) as f:
+        src = f.read()
+
+    def plans(name):
+        n = 0
+        for ln in src[src.index(f"#define {name}(X)"):].split("\n")[1:]:
+            n += ln.strip().startswith("X(")
+            if not ln.rstrip().endswith("\\"):
+                break
+        return n
+
+    assert count.get("k_rows_ct") == plans("PHD_CT_ROWS"), count
+    assert count.get("k_cols_ct") == plans("PHD_CT_COLS"), count
+    assert count.get("k_k1t") == 6, count          # <512, tri> and <1024, tri / full>, x SMALL
+    assert count.get("k_rgb_stats") == 1, count

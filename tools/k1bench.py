@@ -31,7 +31,7 @@ def k1_avg():
     return 1000 * tot.value / max(cnt.value, 1)
 
 
-tag = os.environ.get("PHD_LIB", "default").split("/")[-1] + f" {KIND}" + (f" grid {os.environ['K1GRID']}" if os.environ.get("K1GRID") else "") + (f" form {os.environ['PHD_K1_FORM']}" if os.environ.get("PHD_K1_FORM") else "")
+tag = os.environ.get("PHD_LIB", "default").split("/")[-1] + f" {KIND}" + (f" grid {os.environ['K1GRID']}" if os.environ.get("K1GRID") else "")
 for n, h, w in ([] if os.environ.get("K1ONLY") else [(64, 1080, 1920), (512, 1080, 1920)]):
     t = fill(n, h, w)
     st = (RGB_Statistics * n)()
