@@ -162,11 +162,13 @@ __global__ __launch_bounds__(T) void k_fft_cols(const double2* __restrict__ inte
     // mantissas multiply, exponents add, one fp64 log per run), one atomic per
     // run; the thread's first two runs are logged after the unrolled walk (as
     // fft_ct.hip's walk_runs)
-    unsigned long long* acc = lds_bins ? lb : bin_sums;
     {
         auto flush = [&](int b, double m, int e) {
             const double a = fmax((double)e * 0.69314718055994530942 + log_mant(m, lt), 0.0);
-            if (a > 0.0) atomicAdd(&acc[b], bin_fixed(a, bscale));
+            if (a > 0.0) {
+                if (lds_bins) atomicAdd(&lb[b], bin_fixed(a, bscale));
+                else atomicAdd(&bin_sums[b], bin_fixed(a, bscale));
+            }
         };
         int cur = -1, esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
         double mprod = 1.0, m0 = 1.0, m1 = 1.0;

@@ -65,6 +65,10 @@ constexpr double kWr = 0.299 / 255.0, kWg = 0.587 / 255.0, kWb = 0.114 / 255.0;
 
 // 12 bytes (4 RGB8 pixels) as one dwordx3 register tuple; 4-byte alignment
 typedef unsigned u32x3a __attribute__((ext_vector_type(3), aligned(4)));
+// ... read through a global-address-space pointer: the image pointer comes from
+// a device array, and a generic (flat) load would also count against the LDS
+// counter, so every LDS wait of the FFT would wait for the prefetched pixels
+typedef const __attribute__((address_space(1))) u32x3a gu32x3a;
 
 __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
     const unsigned x = (b >> 2) == 0 ? w.x : ((b >> 2) == 1 ? w.y : w.z);   // b is a constant
@@ -191,8 +195,8 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
 #pragma unroll
         for (int j = 0; j < K::LR; j++) {
             const int g = (K::G4 % T == 0 || tid + j * T < K::G4) ? tid + j * T : 0;
-            rg[j][0] = __builtin_nontemporal_load(reinterpret_cast<const u32x3a*>(r0 + 12 * g));
-            rg[j][1] = __builtin_nontemporal_load(reinterpret_cast<const u32x3a*>(r1 + 12 * g));
+            rg[j][0] = __builtin_nontemporal_load((gu32x3a*)(r0 + 12 * g));
+            rg[j][1] = __builtin_nontemporal_load((gu32x3a*)(r1 + 12 * g));
         }
     };
     int s = 0, im = 0, pr = 0;
@@ -511,13 +515,6 @@ void allow_big_lds(K kernel) {
                               160 * 1024);
 }
 
-// a persistent FFT grid of `full` resident blocks for this call: all of them,
-// or (fft_blocks_per_cu) one per CU when the call runs split over two lanes
-int fft_grid(int full) {
-    const int bpc = fft_blocks_per_cu(), cus = num_cus();
-    return (bpc > 0 && full > bpc * cus) ? bpc * cus : full;
-}
-
 // resident blocks per CU x CUs (the persistent grids)
 template <typename K>
 int resident_grid(K kernel, int threads, size_t lds) {
@@ -532,15 +529,15 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
                    const double2* tw, double2* inter, unsigned long long* rsum, hipStream_t st,
                    const uint8_t* const* imgs = nullptr, int nimg = 1, long istride = 0) {
     const size_t lds = RowK<W, T, Rs...>::lds;
-    static const int full = resident_grid(k_rows_ct<W, T, Rs...>, T, lds);
-    const int g = fft_grid(full) / 32 * 32;                   // schedule needs % 32
-    const int grid = g > 32 ? g : 32;
+    static const int grid = [&] {
+        const int g = resident_grid(k_rows_ct<W, T, Rs...>, T, lds) / 32 * 32;   // schedule needs % 32
+        return g > 32 ? g : 32;
+    }();
     phd_launch((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
                g_ablate, rsum, imgs, nimg, istride);
     return hipGetLastError();
 }
 
-// the resident grid (the most blocks of any call: the max-partial records)
 template <int H, int T, int... Rs>
 int cols_grid() {
     const int g = resident_grid(k_cols_ct<H, T, Rs...>, T, ColK<H, T, Rs...>::lds) / 32 * 32;   // XCD quads
@@ -552,9 +549,7 @@ hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, u
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
                    hipStream_t st, int nimg = 1, long istride = 0, long bstride = 0, long fstride = 0,
                    long sstride = 0) {
-    static const int full = cols_grid<H, T, Rs...>();
-    const int g = fft_grid(full) / 32 * 32;
-    const int grid = g < 32 ? 32 : g;
+    static const int grid = cols_grid<H, T, Rs...>();
     phd_launch((k_cols_ct<H, T, Rs...>), dim3(grid), dim3(T), ColK<H, T, Rs...>::lds, st, inter, wf, cb.runs,
                cb.seg, cb.rstride, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg,
                istride, bstride, fstride, sstride);

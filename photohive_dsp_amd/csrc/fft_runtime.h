@@ -110,8 +110,21 @@ __device__ __forceinline__ int fdiv(int a, int d, float inv) {
     return q;
 }
 
+// LDS pointers for the out-of-line passes: a generic pointer there compiles
+// every LDS access to a flat instruction (slower issue, and it also counts
+// against the vector-memory counter)
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) double2 lds_d2;
+typedef const __attribute__((address_space(3))) double2 lds_cd2;
+typedef const __attribute__((address_space(1))) double2 glb_cd2;
+#else
+typedef double2 lds_d2;            // (the host pass only parses these functions)
+typedef const double2 lds_cd2;
+typedef const double2 glb_cd2;
+#endif
+
 // W_n^e from the two LDS tables (e = 64*hi + lo).
-__device__ __forceinline__ double2 twiddle(const double2* lo, const double2* hi, int e) {
+__device__ __forceinline__ double2 twiddle(lds_cd2* lo, lds_cd2* hi, int e) {
     return cmul(hi[e >> 6], lo[e & 63]);
 }
 
@@ -122,8 +135,7 @@ __device__ __forceinline__ double2 twiddle(const double2* lo, const double2* hi,
 // runs the radix-R DFT, then -- after one barrier -- writes them back.
 // CAP = elements per block the kernel instance supports (8 per thread).
 template <int R, int T>
-__device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns, const double2* lo,
-                                           const double2* hi) {
+__device__ __noinline__ void stockham_pass(lds_d2* buf, int n, int nseq, int Ns, lds_cd2* lo, lds_cd2* hi) {
     constexpr int NB = (8 * T + R * T - 1) / (R * T);
     const int nb = n / R, total = nb * nseq, tstep = n / (Ns * R);
     const float inb = 1.0f / (float)nb, ins = 1.0f / (float)Ns;
@@ -136,7 +148,7 @@ __device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns
         if (t < total) {
             const int seq = nseq == 1 ? 0 : fdiv(t, nb, inb);
             const int j = t - seq * nb;
-            const double2* s = buf + seq * n;
+            lds_cd2* s = buf + seq * n;
 #pragma unroll
             for (int r = 0; r < R; r++) v[b][r] = s[j + r * nb];
             const int jh = fdiv(j, Ns, ins), jm = j - jh * Ns;
@@ -171,8 +183,8 @@ __device__ __noinline__ void stockham_pass(double2* buf, int n, int nseq, int Ns
 
 // Generic radix (any R, incl. a prime length itself): output-parallel direct DFT.
 template <int T>
-__device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns, int R,
-                                          const double2* __restrict__ tw) {
+__device__ __noinline__ void generic_pass(lds_d2* buf, int n, int nseq, int Ns, int R,
+                                          glb_cd2* __restrict__ tw) {
     constexpr int EG = 8;   // outputs per thread (nseq*n <= 8*T)
     const int nb = n / R, total = n * nseq, tstep = n / (Ns * R), nr = n / R;
     double2 out[EG];
@@ -184,7 +196,7 @@ __device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns,
         if (t < total) {
             const int seq = t / n, rem = t - seq * n;
             const int j = rem / R, k = rem - j * R;       // butterfly j, output k
-            const double2* s = buf + seq * n;
+            lds_cd2* s = buf + seq * n;
             const int jm = j % Ns;
             const int step = (jm * tstep + k * nr) % n;   // twiddle exponent per input r (mod n)
             double2 acc = make_double2(0.0, 0.0);
@@ -209,7 +221,10 @@ __device__ __noinline__ void generic_pass(double2* buf, int n, int nseq, int Ns,
 // radix (generic_pass).  A kernel instance holds only the passes its MODE
 // needs (a 16-point pass takes ~150 VGPRs, the small radices ~90).
 template <int T, int MODE>
-__device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan, const double2* lo, const double2* hi) {
+__device__ void fft_lds(double2* buf_, int nseq, const FftPlan& plan, const double2* lo_, const double2* hi_) {
+    lds_d2* buf = (lds_d2*)buf_;                 // (the kernels' extern __shared__ arrays)
+    lds_cd2* lo = (lds_cd2*)lo_;
+    lds_cd2* hi = (lds_cd2*)hi_;
     int Ns = 1;
     for (int p = 0; p < plan.npass; p++) {
         const int R = plan.radix[p];
@@ -227,7 +242,8 @@ __device__ void fft_lds(double2* buf, int nseq, const FftPlan& plan, const doubl
                     if (R == 12) { stockham_pass<12, T>(buf, plan.n, nseq, Ns, lo, hi); break; }
                     if (R == 16) { stockham_pass<16, T>(buf, plan.n, nseq, Ns, lo, hi); break; }
                 }
-                if constexpr ((MODE & 2) != 0) generic_pass<T>(buf, plan.n, nseq, Ns, R, plan.tw);
+                if constexpr ((MODE & 2) != 0)
+                    generic_pass<T>(buf, plan.n, nseq, Ns, R, (glb_cd2*)plan.tw);
                 break;
         }
         Ns *= R;

@@ -46,6 +46,8 @@ namespace {
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) unsigned gu32t;
+// global (not flat) byte loads: a flat load also counts against the LDS counter
+typedef const __attribute__((address_space(1))) uint8_t gu8t;
 
 __device__ __forceinline__ u16x2 as2(unsigned x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ unsigned as1(u16x2 x) { return __builtin_bit_cast(unsigned, x); }
@@ -314,7 +316,8 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         if (last_chunk && tid == 0) {
             // the < 4 pixels of a partial final group
             for (long p = full_end; p < npix; p++) {
-                const int kr = cip[3 * p], kg = cip[3 * p + 1], kb = cip[3 * p + 2];
+                gu8t* pp = (gu8t*)(cip + 3 * p);
+                const int kr = pp[0], kg = pp[1], kb = pp[2];
                 m.sr += kr; m.sg += kg; m.sb += kb;
                 m.qr += kr * kr; m.qg += kg * kg; m.qb += kb * kb;
                 const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 for (int k = lane; k < min(total, kDq); k += 64) {
-                    const uint8_t* q = cip + 3 * (base + (long)dq[k]);
+                    gu8t* q = (gu8t*)(cip + 3 * (base + (long)dq[k]));
                     const int kr = q[0], kg = q[1], kb = q[2];
                     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
                     const K1Px px = k1_exact(kr, kg, kb, code8[code_idx<TRI>(kmx, kmx - kmn)], gp.Lh, k255, G);

@@ -162,12 +162,6 @@ thread_local int t_call_lanes = 1;
 CallLanes::CallLanes(int n) : prev_(t_call_lanes) { t_call_lanes = n; }
 CallLanes::~CallLanes() { t_call_lanes = prev_; }
 
-int fft_blocks_per_cu() {
-    // PHD_FFT_BPC (ablate build): persistent FFT blocks per CU on a split call
-    static const int env = phd_knob("PHD_FFT_BPC") ? atoi(phd_knob("PHD_FFT_BPC")) : 0;
-    return t_call_lanes >= 2 ? env : 0;
-}
-
 int k1_blocks_per_cu() {
     static const int env = phd_knob("PHD_K1_BPC") ? std::max(1, std::min(2, atoi(phd_knob("PHD_K1_BPC")))) : 0;
     // one block per CU only when this call is split over two lanes: the other

@@ -164,9 +164,6 @@ int num_cus();         // compute units of the current device
 // blocks: 7.89k against 7.66k images/s with two lanes, and 6.78k against
 // 7.07k with one, where K1 runs alone; PHD_K1_BPC overrides)
 int k1_blocks_per_cu();
-// Persistent blocks per CU of the compile-time FFT passes on this call (0:
-// as many as are resident)
-int fft_blocks_per_cu();
 // Scope guard: the calling thread's current call runs on n lanes (on_lanes)
 struct CallLanes {
     explicit CallLanes(int n);
