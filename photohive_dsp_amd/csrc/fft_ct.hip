@@ -262,7 +262,10 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
         // i%2); the phantom column WF (odd WF) is 0 (a fixed, unrolled count per
         // thread, branch-free: the next step's wait for its prefetched pixels can
         // then count these stores exactly)
-        double2* orow = inter + im * istride + (size_t)pr * ct_row_stride(W);
+        // (ablation bit 8, timing builds: every block stores to one of 8 fixed
+        // tile rows, so the stores stay L2-resident -- the row-pass FETCH study)
+        double2* orow = inter + ((ablate & 8) ? (size_t)(blockIdx.x & 7) * ct_row_stride(W)
+                                              : im * istride + (size_t)pr * ct_row_stride(W));
         constexpr int NSO = (4 * KP + T - 1) / T;
 #pragma unroll
         for (int j = 0; j < NSO; j++) {
@@ -306,7 +309,7 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     }
 }
 
-template <int H, int T, int... Rs>
+template <int H, int T, bool PFREQ, int... Rs>
 struct ColK {
     using PL = Plan<H, T, 1, Rs...>;
     using L = typename PL::Last;
@@ -321,7 +324,7 @@ struct ColK {
     // the column, the twiddles, log_mant's table, the column's run list and
     // one u64 slot per run (the bins are summed per run, then added to the
     // image's bins column by column: no LDS array of all na x nr bins)
-    static constexpr size_t lds =
+    static constexpr size_t lds_base =
         sizeof(double2) * (H + NTW + kLogTab) + (sizeof(unsigned) + sizeof(unsigned long long)) * kColRunsMax;
     static_assert(Radices<Rs...>::product == H, "plan");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
@@ -329,6 +332,15 @@ struct ColK {
     // CU, one when the column and twiddles fill the LDS
     static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
     static constexpr int MINW = (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2;
+    // The prefetch form (PF, asked for by PFREQ): p per row gets an array of
+    // its own, so the column buffer is free once the last pass has read it,
+    // and the next column streams into it by LDS-DMA (no registers) during the
+    // epilogue -- where it fits beside as many blocks per CU as the plain form
+    // (3000 and 2000 rows: two; 6000: one).  4000 rows would drop to one
+    // block: plain form only.
+    static constexpr size_t lds_pf = lds_base + sizeof(double) * H;
+    static constexpr bool PF = PFREQ && lds_pf * BPC1 <= 160 * 1024;
+    static constexpr size_t lds = PF ? lds_pf : lds_base;
 };
 
 // One column per block: blocks b, b^8, b^16, b^24 (one XCD) take the four
@@ -336,8 +348,33 @@ struct ColK {
 // into that XCD's L2 (the grid is a multiple of 32).  A step's tiles are
 // loaded at its start; the other blocks of the CU hide the latency (round 3:
 // prefetching the next column into registers measured slower, it cost VGPRs).
-template <int H, int T, int... Rs>
-__global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
+// One 16-byte LDS-DMA per lane: global g -> LDS at the wave's base + lane x 16
+// (global_load_lds_dwordx4; M0 holds the wave-uniform LDS base).  Inline asm
+// rather than the builtin: the compiler would make every later LDS read wait
+// for the DMA (it cannot tell the regions apart), draining the prefetch at
+// the epilogue's first read; the kernel waits for it itself (vmcnt, then a
+// barrier) before the buffer is read.
+__device__ __forceinline__ void lds_dma16(const void* g, void* lds_wave_base) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned m = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds_wave_base);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(m)
+                 : "memory");
+#else
+    (void)g;
+    (void)lds_wave_base;
+#endif
+}
+
+// every vector memory operation of the wave done (vmcnt(0); expcnt, lgkmcnt
+// left alone): a DMA-filled buffer may be read after this and a barrier
+__device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+template <int H, int T, bool PFREQ, int... Rs>
+__global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
                                                      const unsigned* __restrict__ runs,
                                                      const uint8_t* __restrict__ segidx, int rstride,
                                                      unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
@@ -345,7 +382,7 @@ __global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const 
                                                      const unsigned long long* __restrict__ sums0, int width,
                                                      double* __restrict__ dbg, double bscale, int ablate_arg,
                                                      int nimg, long istride, long bstride, long fstride, long sstride) {
-    using K = ColK<H, T, Rs...>;
+    using K = ColK<H, T, PFREQ, Rs...>;
     const int ablate = PHD_ABL(ablate_arg);
     using L = typename K::L;
     constexpr int R = K::R;
@@ -355,6 +392,9 @@ __global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const 
     double2* lt = tw + K::NTW;                                 // log_mant's table
     unsigned long long* sl = reinterpret_cast<unsigned long long*>(lt + kLogTab);   // [kColRunsMax]
     unsigned* rl = reinterpret_cast<unsigned*>(sl + kColRunsMax);                   // [kColRunsMax]
+    // p per spectrum row: its own array in the prefetch form, else the
+    // column buffer (free once the last pass has read it)
+    double* lgb = K::PF ? reinterpret_cast<double*>(rl + kColRunsMax) : reinterpret_cast<double*>(buf);
     const int tid = threadIdx.x;
     // a batch: nimg images of one size, their intermediates, bin sums, max
     // partials and channel sums istride / bstride / fstride / sstride apart;
@@ -386,6 +426,21 @@ __global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const 
     // loads its column's 32-B half of tiles (row pair tid/2, row tid%2), as raw
     // 16-byte words that land in the registers the LDS stores read
     const int prow0 = tid / 2, psub = 2 * half + (tid & 1);
+    // the column of step u into the buffer by LDS-DMA (PF): element 2 prow0 +
+    // (tid & 1) + c T is lane-linear, the wave's base + lane x 16 B
+    auto dma = [&](int u) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(inter) + (size_t)prow0 * rs + (size_t)pair_at(u) * 4 + psub;
+#pragma unroll 1
+        for (int c = 0; c < K::CR; c++) {
+            const int pr = min(c * (T / 2), K::P - 1 - prow0);
+            const int y = 2 * (prow0 + c * (T / 2)) + (psub & 1);
+            if (((2 * K::P) % T == 0 || tid + c * T < 2 * K::P) && (H % 2 == 0 || y < H))
+                lds_dma16(src + (size_t)pr * rs, buf + (tid & ~63) + c * T);
+        }
+    };
+    // (ablation bit 32, timing builds: the prefetch form loads each column at
+    // its own step instead, i.e. synchronously)
+    const bool pf_late = (ablate & 32) != 0;
     // (a block without units still runs one empty segment: its max partial and
     // bins are written as the one-image form always did)
     for (int seg = c0, im = c0 / nunit, first = 1; first || seg < c1; im++, first = 0) {
@@ -398,9 +453,13 @@ __global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const 
     sums = sums0 + im * sstride;
     double mx = 0.0;
     __syncthreads();
+    if (K::PF && u0 < un && !pf_late) dma(u0);
     for (int u = u0; u < un; u++) {
         const int kp = pair_at(u);
-        {
+        if (K::PF) {
+            if (pf_late) dma(u);
+            wait_vmem();                          // this wave's DMA of the column is in LDS
+        } else {
             u32x4 pf[K::CR];
             const u32x4* src = reinterpret_cast<const u32x4*>(inter) + (size_t)prow0 * rs + (size_t)kp * 4 + psub;
 #pragma unroll
@@ -454,8 +513,12 @@ __global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const 
             L::load(buf, v, tid);
             L::compute(v, tw + K::PL::last_tw_offset, tid);
         }
-        __syncthreads();                       // every thread has read its last-pass inputs
-        double* lgb = reinterpret_cast<double*>(buf);   // p per spectrum row, 1 for p < 1 (log 0)
+        // PF: nothing waits for the buffer after the last pass's reads, so p, the
+        // run list and the barrier come first and the next column's DMA is
+        // issued behind them (the walk and the atomics run while it lands);
+        // plain: the barrier first, p then overwrites the buffer
+        if (!K::PF) __syncthreads();               // every thread has read its last-pass inputs
+        // lgb: p per spectrum row, 1 for p < 1 (log 0)
 #pragma unroll
         for (int q = 0; q < L::ROUNDS; q++) {
             const int b = tid + q * T;
@@ -473,7 +536,11 @@ __global__ __launch_bounds__(T, (ColK<H, T, Rs...>::MINW)) void k_cols_ct(const 
 #pragma unroll
         for (int k = 0; k < K::RPT; k++)
             if (tid + k * T < kColRunsMax) rl[tid + k * T] = rreg[k];
+        // PF: the run loads (and any debug stores) retire before a DMA is in
+        // flight, so no later wait of the compiler's counts the DMA
+        if (K::PF) wait_vmem();
         __syncthreads();
+        if (K::PF && u + 1 < un && !pf_late) dma(u + 1);
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
         if (!(ablate & 2)) walk_runs<K::E>(lgb, tid * K::E, H, rl, sidx, sl, bscale, lt);
@@ -538,22 +605,48 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
     return hipGetLastError();
 }
 
-template <int H, int T, int... Rs>
-int cols_grid() {
-    const int g = resident_grid(k_cols_ct<H, T, Rs...>, T, ColK<H, T, Rs...>::lds) / 32 * 32;   // XCD quads
+template <int H, int T, bool PF, int... Rs>
+int cols_grid_form() {
+    const int g = resident_grid(k_cols_ct<H, T, PF, Rs...>, T, ColK<H, T, PF, Rs...>::lds) / 32 * 32;   // XCD quads
     return g < 32 ? 32 : g;
 }
 
+// the max partials per image: the larger of the two forms' grids (a form with
+// fewer blocks leaves its slots at the workspace's zero)
+template <int H, int T, int... Rs>
+int cols_grid() {
+    static const int g = [] {
+        int a = cols_grid_form<H, T, false, Rs...>();
+        if constexpr (ColK<H, T, true, Rs...>::PF) a = std::max(a, cols_grid_form<H, T, true, Rs...>());
+        return a;
+    }();
+    return g;
+}
+
+template <int H, int T, bool PF, int... Rs>
+hipError_t cols_ct_form(const double2* inter, int width, int wf, const ColBins& cb, unsigned long long* bin_sums,
+                        double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
+                        hipStream_t st, int nimg, long istride, long bstride, long fstride, long sstride) {
+    static const int grid = cols_grid_form<H, T, PF, Rs...>();
+    phd_launch((k_cols_ct<H, T, PF, Rs...>), dim3(grid), dim3(T), ColK<H, T, PF, Rs...>::lds, st, inter, wf,
+               cb.runs, cb.seg, cb.rstride, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate,
+               nimg, istride, bstride, fstride, sstride);
+    return hipGetLastError();
+}
+
+// pf: the prefetch form where the plan has one (FftSel::col_pf)
 template <int H, int T, int... Rs>
 hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, unsigned long long* bin_sums,
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,
-                   hipStream_t st, int nimg = 1, long istride = 0, long bstride = 0, long fstride = 0,
+                   hipStream_t st, bool pf, int nimg = 1, long istride = 0, long bstride = 0, long fstride = 0,
                    long sstride = 0) {
-    static const int grid = cols_grid<H, T, Rs...>();
-    phd_launch((k_cols_ct<H, T, Rs...>), dim3(grid), dim3(T), ColK<H, T, Rs...>::lds, st, inter, wf, cb.runs,
-               cb.seg, cb.rstride, bin_sums, fmax_part, tw, sums, width, dbg, bin_scale(H, wf), g_ablate, nimg,
-               istride, bstride, fstride, sstride);
-    return hipGetLastError();
+    if constexpr (ColK<H, T, true, Rs...>::PF) {
+        if (pf)
+            return cols_ct_form<H, T, true, Rs...>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, dbg, st,
+                                                   nimg, istride, bstride, fstride, sstride);
+    }
+    return cols_ct_form<H, T, false, Rs...>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, dbg, st, nimg,
+                                            istride, bstride, fstride, sstride);
 }
 
 // log_mant over an array (tests: its accuracy against the host's log)
@@ -605,7 +698,7 @@ int fft_cols_ct_threads(int h) {
 
 size_t fft_cols_ct_lds(int h) {
 #define PHD_X(N, T, ...) \
-    if (h == N) return ColK<N, T, __VA_ARGS__>::lds;
+    if (h == N) return ColK<N, T, false, __VA_ARGS__>::lds;
     PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return 0;
@@ -644,11 +737,11 @@ hipError_t launch_fft_rows_ct_batch(const uint8_t* const* d_imgs, int n, int hei
 hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int n, int height, int width, int wf,
                                     const ColBins& cb, unsigned long long* bin_sums, long bin_stride,
                                     double* fmax_part, long fmax_stride, const double2* tw,
-                                    const unsigned long long* sums, long sums_stride, hipStream_t st) {
+                                    const unsigned long long* sums, long sums_stride, hipStream_t st, bool pf) {
     if (n < 1) return hipErrorInvalidValue;
 #define PHD_X(N, T, ...)                                                                                       \
     if (height == N)                                                                                           \
-        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, nullptr, st, n, \
+        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, nullptr, st, pf, n, \
                                           inter_stride, bin_stride, fmax_stride, sums_stride);
     PHD_CT_COLS(PHD_X)
 #undef PHD_X
@@ -657,10 +750,10 @@ hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int
 
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const ColBins& cb,
                               unsigned long long* bin_sums, double* fmax_part, const double2* tw,
-                              const unsigned long long* sums, double* dbg, hipStream_t st) {
+                              const unsigned long long* sums, double* dbg, hipStream_t st, bool pf) {
 #define PHD_X(N, T, ...) \
     if (height == N)     \
-        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, dbg, st);
+        return cols_ct<N, T, __VA_ARGS__>(inter, width, wf, cb, bin_sums, fmax_part, tw, sums, dbg, st, pf);
     PHD_CT_COLS(PHD_X)
 #undef PHD_X
     return hipErrorInvalidValue;

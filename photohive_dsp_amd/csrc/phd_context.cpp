@@ -391,7 +391,8 @@ hipError_t launch_cols_sel(const FftSel& s, const double2* inter, int height, in
                            const unsigned long long* sums, double* dbg, hipStream_t st) {
     if (s.ct) {
         if (!s.cbins.runs) return hipErrorInvalidValue;   // select_fft without a table
-        return launch_fft_cols_ct(inter, height, width, wf, s.cbins, bin_sums, fmax_part, s.tw_c, sums, dbg, st);
+        return launch_fft_cols_ct(inter, height, width, wf, s.cbins, bin_sums, fmax_part, s.tw_c, sums, dbg, st,
+                                  s.col_pf);
     }
     if (dbg) return hipErrorNotSupported;
     if (s.generic) return generic_cols(s, const_cast<double2*>(inter), height, wf, binmap, nbins, bin_sums, fmax_part, st);

@@ -283,6 +283,10 @@ struct FftSel {
     const double2* tw_c = nullptr;
     int col_blocks = 0;   // entries of the per-block max partials
     ColBins cbins;        // compile-time column pass: its per-column polar-bin runs
+    // compile-time column pass: its prefetch form (the next column streams into
+    // LDS during the epilogue) where the plan has one; run_reports turns it off
+    // when another lane's two-block K1 shares the CUs (measured)
+    bool col_pf = true;
     // the generic path (a side above the LDS limit or with a large prime
     // factor): row pairs -> global row transforms -> split / transpose, then
     // the fused runtime column pass (cols_fused) or global column transforms

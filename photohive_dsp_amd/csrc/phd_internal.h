@@ -351,7 +351,7 @@ hipError_t launch_fft_rows_ct(const uint8_t* img, int height, int width, const u
 // dbg (optional): the power spectrum, column-major [wf][height]
 hipError_t launch_fft_cols_ct(const double2* inter, int height, int width, int wf, const ColBins& cb,
                               unsigned long long* bin_sums, double* fmax_part, const double2* tw,
-                              const unsigned long long* sums, double* dbg, hipStream_t st);
+                              const unsigned long long* sums, double* dbg, hipStream_t st, bool pf = true);
 // Batches of n images of one size in one launch each (sizes whose row pairs
 // form whole line groups, (height + 1) / 2 % 4 == 0): d_imgs is a device array
 // of image pointers; image i's intermediate, bin sums, max partials and channel
@@ -362,7 +362,8 @@ hipError_t launch_fft_rows_ct_batch(const uint8_t* const* d_imgs, int n, int hei
 hipError_t launch_fft_cols_ct_batch(const double2* inter, long inter_stride, int n, int height, int width, int wf,
                                     const ColBins& cb, unsigned long long* bin_sums, long bin_stride,
                                     double* fmax_part, long fmax_stride, const double2* tw,
-                                    const unsigned long long* sums, long sums_stride, hipStream_t st);
+                                    const unsigned long long* sums, long sums_stride, hipStream_t st,
+                                    bool pf = true);
 // Same, the luma from an fp64 plane when pgm != nullptr (planar input).
 hipError_t launch_sharpness_src(const uint8_t* img, const double* pgm, int height, int width, int n, const int* top,
                                 const int* bottom, const int* left, const int* right, const double* k255,

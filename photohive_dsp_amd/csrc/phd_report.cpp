@@ -489,6 +489,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (!select_fft(c, height, width, nbins, d_imgs, n, &fs, tbl, ct_batchable)) return false;
     const Context::Cls* cls = get_cls(c, gp);
     if (!cls) return false;
+    // the column pass's prefetch form holds ~24 KB more LDS per block: on a
+    // call split over two lanes whose K1 runs the two-block form (one 512-thread
+    // block per CU beside the other lane's FFTs) it measured 3 % slower
+    // (8.67k against 8.95k images/s at 4000x3000, 18/2/3), where FFT-only
+    // calls and the fine grids' one-block K1 gain 3 %
+    if (ds <= 1 && k1_blocks_per_cu() == 1 && cls->fc.k1t_cshift2 >= 0) fs.col_pf = false;
 
     const int ncolblocks = fs.col_blocks;
     // images whose result records go to the host together (one event and one
@@ -549,8 +555,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (!k1_ok) return false;
     if (k1_own && !k1_rec) PHD_HIP(hipEventRecord(c->ev[0], st));   // (a K1 path without phd_launch: timing only)
     if (!k1_rec) PHD_HIP(hipEventRecord(c->ev[1], st));
-    const hipEvent_t ev_k1 = k1_rec ? c->ev[1] : c->ev_k1;
     if (!k1_rec) PHD_HIP(hipEventRecord(c->ev_k1, st));
+    const hipEvent_t ev_k1 = k1_rec ? c->ev[1] : c->ev_k1;
     // the A records go down on the side stream (tail), beside the FFTs
     const hipStream_t sa = k1_rec ? c->tail : st;
     if (sa != st) PHD_HIP(hipStreamWaitEvent(sa, ev_k1, 0));
@@ -596,7 +602,7 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
                                          (unsigned long long*)(dw + L.C(n, g0) + L.c_bins), (long)(L.c_bytes / 8),
                                          (double*)(dw + L.C(n, g0) + L.c_fmax), (long)(L.c_bytes / 8), fs.tw_c,
                                          (const unsigned long long*)(dw + L.A(g0) + L.a_sums), (long)(L.a_bytes / 8),
-                                         sf));
+                                         sf, fs.col_pf));
         c->prof.end(ps, sf);
         for (int i = g0; i < g1; i++) {
             if (ncrops)

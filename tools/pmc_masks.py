@@ -1,6 +1,7 @@
 """FETCH_SIZE / WRITE_SIZE of one FFT pass under ablation masks (run ON the
 GPU box, ablate build): which part of the pass causes which memory traffic.
     python tools/pmc_masks.py KERNEL MASK [MASK ...]   (KERNEL 1 rows, 2 cols)
+    (PMC_COUNTERS="TCC_EA0_RDREQ_sum ..." for other counters, one pass each)
 -> gpurun_out/pmc_masks_K.json; per mask the average counter per launch of
 tools/kbench.py's 20 timed launches (the first launch of each mask, the
 setup report's, is dropped)."""
@@ -36,12 +37,14 @@ def main():
     kernel = int(sys.argv[1])
     masks = [int(m) for m in sys.argv[2:]]
     res = {"kernel": NAME[kernel], "masks": {}}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    # PMC_COUNTERS="A B ...": other counters, one pass each (default the two sizes)
+    for counter in os.environ.get("PMC_COUNTERS", "FETCH_SIZE WRITE_SIZE").split():
         v = run(counter, kernel, masks)
         per = len(v) // len(masks) if masks else 0     # launches per mask (setup report + 20 timed)
         for i, m in enumerate(masks):
             part = v[i * per:(i + 1) * per][1:]
-            res["masks"].setdefault(str(m), {})[counter + "_kb_avg"] = sum(part) / max(len(part), 1)
+            key = counter + ("_kb_avg" if counter.endswith("_SIZE") else "_avg")
+            res["masks"].setdefault(str(m), {})[key] = sum(part) / max(len(part), 1)
             res["masks"][str(m)]["launches"] = len(part)
     with open(os.path.join(ROOT, "gpurun_out", f"pmc_masks_{kernel}.json"), "w") as fh:
         json.dump(res, fh, indent=1)
