@@ -84,8 +84,7 @@ Context* get_context_lane(int lane) {
         hipEventCreateWithFlags(&c->ev_tail, of) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_dl_sd, of) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fft, of) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_null, of) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_gate, of) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_null, of) != hipSuccess) {
         set_error("hipStreamCreate failed");
         delete c;
         return nullptr;

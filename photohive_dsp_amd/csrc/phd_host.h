@@ -212,7 +212,6 @@ struct Context {
     std::vector<hipEvent_t> ev_img_fft, ev_img_dl;
     KernelProfiler prof;
     hipEvent_t ev_null = nullptr;                   // orders the library stream after the null stream
-    hipEvent_t ev_gate = nullptr;                   // lane 0's K1 end, for lane 1 (K1Gate, phd_report.cpp)
     // host-buffer uploads (phd_upload.cpp): pinned slot ring on the h2d stream,
     // two device staging buffers for overlapping groups
     hipStream_t h2d = nullptr;

@@ -18,7 +18,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <unistd.h>
@@ -443,43 +442,9 @@ bool fused_slot_sums(const GridParams& gp, const PaletteDecision& dec, const uns
     return true;
 }
 
-// K1 gate of a call split over two lanes: lane 1's K1 starts on the GPU after
-// lane 0's K1 has finished (an event lane 0 records behind its K1, which lane
-// 1's stream waits for), so lane 1 classifies beside lane 0's FFTs instead of
-// two K1s sharing the CUs at the start of every call.
-struct K1Gate {
-    hipEvent_t ev = nullptr;       // lane 0's K1 end (recorded when state == 1)
-    std::mutex m;
-    std::condition_variable cv;
-    int state = 0;                 // 0 closed, 1 event recorded, 2 open without an event
-    void open(int how) {
-        {
-            std::lock_guard<std::mutex> lk(m);
-            if (state) return;
-            state = how;
-        }
-        cv.notify_all();
-    }
-    int wait() {
-        std::unique_lock<std::mutex> lk(m);
-        cv.wait(lk, [&] { return state != 0; });
-        return state;
-    }
-};
-namespace {
-thread_local K1Gate* t_gate = nullptr;   // the gate of this thread's lane call
-thread_local int t_gate_role = 0;        // 1: lane 0 opens it, 2: lane 1 waits
-}
-
 bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, int width,
                  const phd_config& cfg, const Crop_Boundaries* crops, Full_Report_Data** out, int* status,
                  hipStream_t stream) {
-    // lane 0: whatever happens, the gate opens when this call returns
-    struct GateGuard {
-        ~GateGuard() {
-            if (t_gate && t_gate_role == 1) t_gate->open(2);
-        }
-    } gate_guard;
     const auto t_host0 = std::chrono::steady_clock::now();
     for (int i = 0; i < n; i++) {
         out[i] = nullptr;
@@ -582,12 +547,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     static const bool k1_events_off = phd_knob("PHD_K1_MARKERS") != nullptr;
     const bool k1_own = ds <= 1 && !(c->prof.mask & (1u << kK1)) && !k1_events_off &&
                         device_event_flags() == hipEventDisableSystemFence;
-    if (t_gate && t_gate_role == 2 && t_gate->wait() == 1) PHD_HIP(hipStreamWaitEvent(st, t_gate->ev, 0));
     if (k1_own) launch_events() = LaunchEvents{c->ev[0], c->ev[1], false};
     else PHD_HIP(hipEventRecord(c->ev[0], st));
     const bool k1_ok = launch_k1(c, L, n, d_imgs, height, width, ds, gp, cls, nchunks, fused, st);
-    if (k1_ok && t_gate && t_gate_role == 1 && t_gate->ev && hipEventRecord(t_gate->ev, st) == hipSuccess)
-        t_gate->open(1);
     const bool k1_rec = k1_own && launch_events().used;
     if (k1_own) launch_events() = LaunchEvents{};
     if (!k1_ok) return false;
@@ -1178,21 +1140,11 @@ extern "C" int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int h
     // two lanes for large batches on the library's streams: the second half on
     // lane 1, so each half's host phases and launch gaps overlap the other's
     // kernels
-#ifndef PHD_LANE_STAGGER
-#define PHD_LANE_STAGGER 0
-#endif
-    K1Gate gate;
-    // (lane 0 is this device's first context: its event, recorded under its lock)
-    if (PHD_LANE_STAGGER) gate.ev = c->ev_gate;
     on_lanes(c, n_images >= 16 && !stream, [&](Context* cl, int lane, int nl) {
         const int h = nl == 2 ? n_images / 2 : n_images;
         const int i0 = lane ? h : 0, m = lane ? n_images - h : h;
-        t_gate = (PHD_LANE_STAGGER && nl == 2 && gate.ev) ? &gate : nullptr;
-        t_gate_role = lane ? 2 : 1;
         run_reports(cl, imgs.data() + i0, m, height, width, *cfg, nullptr, out + i0, status + i0,
                     (hipStream_t)stream);
-        t_gate = nullptr;
-        t_gate_role = 0;
     });
     int fails = 0;
     for (int i = 0; i < n_images; i++) fails += status[i] != 0;
