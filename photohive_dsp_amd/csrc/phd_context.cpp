@@ -326,9 +326,16 @@ const double2* get_ct_twiddles(Context* c, int n, bool rows) {
 
 // batch: the caller will run the compile-time passes as batched launches
 // (one row and one column launch per group of same-size images)
+namespace {
+std::atomic<int> g_column_form{-1};
+}
+
+int FftSel::forced_form() { return g_column_form.load(std::memory_order_relaxed); }
+
 bool select_fft(Context* c, int height, int width, int nbins, const uint8_t* const* imgs, int n, FftSel* s,
                 const BlurTable* tbl, bool batch) {
     *s = FftSel{};
+    if (FftSel::forced_form() >= 0) s->col_pf = FftSel::forced_form() == 1;
     static const bool force_generic = phd_knob("PHD_FFT_GENERIC") != nullptr;   // A/B experiments only
     bool ct = !force_generic && ct_rows_plan(width, nullptr) && ct_cols_plan(height, nullptr) &&
               fft_cols_ct_lds(height) <= 160 * 1024;
@@ -576,4 +583,8 @@ extern "C" int phd_device_info(char* buf, int buflen) {
         snprintf(buf, buflen, "%s %s CUs=%d HBM=%.1fGB", pr.name, pr.gcnArchName, pr.multiProcessorCount,
                  pr.totalGlobalMem / 1e9);
     return dev;
+}
+
+extern "C" int phd_debug_column_form(int mode) {
+    return phd::g_column_form.exchange(mode < 0 ? -1 : (mode ? 1 : 0));
 }

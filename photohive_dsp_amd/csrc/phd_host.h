@@ -287,6 +287,8 @@ struct FftSel {
     // LDS during the epilogue) where the plan has one; run_reports turns it off
     // when another lane's two-block K1 shares the CUs (measured)
     bool col_pf = true;
+    // phd_debug_column_form: -1 the library's choice, 0 plain, 1 prefetch form
+    static int forced_form();
     // the generic path (a side above the LDS limit or with a large prime
     // factor): row pairs -> global row transforms -> split / transpose, then
     // the fused runtime column pass (cols_fused) or global column transforms

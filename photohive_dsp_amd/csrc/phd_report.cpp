@@ -494,7 +494,8 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // lane's FFTs) it measured 3 % slower (8.67k against 8.95k images/s at
     // 4000x3000, 18/2/3), where FFT-only calls and the fine grids' one-block
     // K1 gain 3 %
-    if (ds <= 1 && k1_blocks_per_cu() == 1 && cls->fc.k1t_cshift2 >= 0) fs.col_pf = false;
+    if (FftSel::forced_form() < 0 && ds <= 1 && k1_blocks_per_cu() == 1 && cls->fc.k1t_cshift2 >= 0)
+        fs.col_pf = false;
 
     const int ncolblocks = fs.col_blocks;
     // images whose result records go to the host together (one event and one

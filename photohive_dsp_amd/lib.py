@@ -101,6 +101,8 @@ lib.phd_debug_log_mant.restype = ctypes.c_int
 lib.phd_debug_log_mant.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
 lib.phd_debug_col_runs_max.restype = ctypes.c_int
 lib.phd_debug_col_runs_max.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+lib.phd_debug_column_form.restype = ctypes.c_int
+lib.phd_debug_column_form.argtypes = [ctypes.c_int]
 lib.phd_debug_gfft.restype = ctypes.c_int
 lib.phd_debug_gfft.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_long]
 lib.free_full_report.restype = None

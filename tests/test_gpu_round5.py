@@ -1,7 +1,8 @@
 """Round-5 GPU tests: two library lanes on eight HIP hardware queues in a fresh
-process (the bench's default configuration), and the compile-time size whose
+process (the bench's default configuration), the compile-time size whose
 polar-bin table has too many runs per column for the column pass's run lists
-(the runtime-plan fallback) against the oracle."""
+(the runtime-plan fallback) against the oracle, and the column pass's two
+forms (plain and LDS-DMA prefetch) against each other."""
 import ctypes
 import json
 import os
@@ -52,3 +53,37 @@ def test_column_runs_fallback_4000x3000_against_oracle():
     for _ in range(2):
         rep = phd.get_report(img, radius_partitions=160)
         assert_report_matches(rep, g)
+
+
+# (height, width): every compile-time column plan with a prefetch form, each
+# with a compile-time row plan for its width
+PF_SIZES = [(3000, 4000), (2000, 3000), (6000, 4000), (1536, 2048), (1080, 1920), (1280, 720),
+            (720, 1280), (640, 480), (480, 640), (512, 512)]
+
+
+@pytest.mark.parametrize("h,w", PF_SIZES)
+def test_column_forms_bit_identical(h, w):
+    """The compile-time column pass's plain form and its LDS-DMA prefetch form
+    (phd_debug_column_form) give the same bins, max and blur vectors for a
+    batch (the polar bins are fixed-point sums: bit-identical whatever the
+    order), on one lane and, at the default lanes, for a split batch."""
+    phd, L, torch = _phd()
+    n = 4 if h * w >= 6_000_000 else 6
+    # generated on the device (synth.hip): uniform and blurred structured images
+    t = torch.empty((n, h, w, 3), dtype=torch.uint8, device="cuda")
+    for i in range(n):
+        p = t[i].data_ptr()
+        rc = (L.lib.phd_fill_uniform_device(p, h * w * 3, 900 + i, None) if i % 2 == 0 else
+              L.lib.phd_fill_structured_device(p, h, w, 900 + i, 15, 1, None))
+        assert rc == 0
+    prev = L.lib.phd_debug_column_form(0)
+    try:
+        plain = phd.report_device(t)
+        assert L.lib.phd_debug_column_form(1) == 0
+        pf = phd.report_device(t)
+    finally:
+        L.lib.phd_debug_column_form(prev)
+    for a, b in zip(plain, pf):
+        assert np.array_equal(np.array(a.blur_profile.bins), np.array(b.blur_profile.bins))
+        assert [(v.angle, v.magnitude) for v in a.blur_vectors] == [(v.angle, v.magnitude) for v in b.blur_vectors]
+        assert a.color_palette.group_ids == b.color_palette.group_ids

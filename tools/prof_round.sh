@@ -4,8 +4,8 @@
 # rocprofv3 kernel statistics of config 2 alone and of the default bench
 # command, and the default bench line.  Stops at the first crash / timeout
 # (tools/gpu_run.sh).  Copy the results into profiles/rNN/.
-#   bash tools/prof_round.sh r04 [steps...]   (steps: tests k1 calib pmc prof bench; default all)
-TAG="${1:-r04}"; shift
+#   bash tools/prof_round.sh r05 [steps...]   (steps: tests k1 calib pmc prof bench; default all)
+TAG="${1:-r05}"; shift
 STEPS="${*:-tests k1 calib pmc prof bench}"
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -17,7 +17,7 @@ for s in $STEPS; do
     calib) args+=("pmc_calib:400:python tools/pmc_calib.py");;
     pmc) args+=("pmc_collect:400:python tools/pmc_collect.py --tag $TAG -- --steps 3 --warmup 1 --no-configs --batch 8");;
     prof) args+=("prof_config2:400:GPU_MAX_HW_QUEUES=8 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof2 -o prof -- python bench.py --no-configs --no-cpu-baseline --lanes 1"
-                 "prof_default:500:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline --hw-queues 0");;
+                 "prof_default:500:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o prof -- python bench.py --no-cpu-baseline --hw-queues 8");;
     bench) args+=("bench_full:500:python bench.py");;
   esac
 done
