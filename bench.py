@@ -52,9 +52,9 @@ def parse(argv=None):
                         "headline roofline is the whole pipeline's and one_lane repeats the headline on one "
                         "lane, where each launch of the dominant kernel runs alone and its events price it")
     p.add_argument("--hw-queues", type=int, default=8,
-                   help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; 0 keeps the environment's): "
-                        "two lanes use 8 HIP streams, and with HIP's default of 4 hardware queues pairs of them share "
-                        "a queue and serialise (round 4: 8.32k images/s with 4, 8.81k with 8)")
+                   help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; 0 keeps the environment's, "
+                        "where the package's own default is 8): two lanes drive 4 HIP streams beside HIP's copy "
+                        "traffic (round 5: 8.60-8.77k images/s with HIP's 4 queues, 8.87-8.97k with 8)")
     p.add_argument("--no-one-lane", action="store_true",
                    help="skip the one-lane repeat of the headline (one_lane)")
     p.add_argument("--height", type=int, default=3000)

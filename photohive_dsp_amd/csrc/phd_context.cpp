@@ -327,7 +327,10 @@ const double2* get_ct_twiddles(Context* c, int n, bool rows) {
 // batch: the caller will run the compile-time passes as batched launches
 // (one row and one column launch per group of same-size images)
 namespace {
-std::atomic<int> g_column_form{-1};
+#ifndef PHD_COLUMN_FORM
+#define PHD_COLUMN_FORM -1   // (A/B variant builds: the initial phd_debug_column_form)
+#endif
+std::atomic<int> g_column_form{PHD_COLUMN_FORM};
 }
 
 int FftSel::forced_form() { return g_column_form.load(std::memory_order_relaxed); }

@@ -21,6 +21,13 @@ def _preload_torch_hip_runtime():
         ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
 
 
+# The two library lanes drive four HIP streams beside HIP's own copy traffic;
+# eight hardware queues measured +2-4 % images/s over HIP's default four
+# (DESIGN.md section 12).  HIP reads the variable once, when its runtime
+# initialises, so it is set here, before this package's first HIP call, and
+# only when the process has not chosen a value (a HIP runtime that is
+# already initialised, e.g. by earlier torch.cuda work, keeps its queues).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 _preload_torch_hip_runtime()
 directory = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.path.join(directory, "PhotoHive_DSP_lib/libreport_data.so")
