@@ -860,6 +860,9 @@ def main(argv=None):
         if args.cpu_procs:
             topo["procs_reason"] = f"--cpu-procs {args.cpu_procs}"
         cpu = cpu_baseline(args.height, args.width, topo, procs)
+    # the package before torch: it sets GPU_MAX_HW_QUEUES (when unset) ahead of
+    # HIP's initialisation (--hw-queues 0 then runs on the package's default)
+    import photohive_dsp_amd  # noqa: F401
     import torch
     ndev = torch.cuda.device_count()
     dev = local % ndev if ndev else local
@@ -870,7 +873,6 @@ def main(argv=None):
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-    import photohive_dsp_amd  # noqa: F401
     cx = Ctx(args, world, rank, backend)
     dump_maps("ctx")
 
