@@ -463,6 +463,10 @@ def headline(cx, timed_events=True, kind="uniform", steps=None):
     warm_alone = warm
     if lanes > 1 and cand:
         lib.phd_set_lanes(1)
+        # one untimed step first: a one-lane call may launch kernel forms the
+        # two-lane steps did not (the column pass's prefetch form), whose
+        # first launches load their code
+        step()
         warm_alone = time_candidates()
         lib.phd_set_lanes(lanes)
         step()
