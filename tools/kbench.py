@@ -6,7 +6,7 @@ import torch
 torch.cuda.set_device(0)
 from photohive_dsp_amd.lib import lib, last_error
 from photohive_dsp_amd.core import make_config
-H, W = 3000, 4000
+H, W = (int(x) for x in os.environ.get("KB_SIZE", "3000x4000").split("x"))   # KB_SIZE=HxW
 n = H * W * 3
 img = torch.empty(n, dtype=torch.uint8, device="cuda")
 assert lib.phd_fill_uniform_device(img.data_ptr(), n, 1, None) == 0
