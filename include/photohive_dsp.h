@@ -244,8 +244,8 @@ int phd_debug_log_mant(const double* d_x, double* d_y, long n);
  * the runtime-plan FFT.  Returns the count or -1. */
 int phd_debug_col_runs_max(int height, int width, int radius_partitions, int angle_partitions);
 /* Test hook: the compile-time column pass's form for later calls of this
- * process: -1 the library's choice (default), 0 the plain form, 1 the
- * LDS-DMA prefetch form where the plan has one.
+ * process: -1 the library's choice (default), 0 the half-prefetch form, 1 the
+ * full-prefetch form where the plan has one.
  * Returns the previous setting. */
 int phd_debug_column_form(int mode);
 

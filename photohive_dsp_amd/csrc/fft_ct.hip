@@ -28,7 +28,8 @@
 // Column kernel (persistent, two blocks of T threads per CU, one column at a
 // time per block; blocks b, b^8, b^16, b^24 of one XCD take the four columns
 // of the same 128-byte lines, each block a contiguous range of line pairs).
-// The next column is prefetched into registers.
+// The next column streams into LDS by LDS-DMA while the current one finishes
+// (the full- or half-prefetch form, ColK).
 // The last pass's outputs never go back to LDS as spectra: the epilogue forms
 // p = re^2 + im^2, keeps the block's max and writes p (1 for p < 1, whose log
 // the reference clamps away) per spectrum row to LDS; each thread then walks a
@@ -309,7 +310,9 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     }
 }
 
-template <int H, int T, bool PFREQ, int... Rs>
+// FULL: the full-prefetch form (p in an LDS array of its own), else the
+// half-prefetch form (p in the lower half of the column buffer)
+template <int H, int T, bool FULL, int... Rs>
 struct ColK {
     using PL = Plan<H, T, 1, Rs...>;
     using L = typename PL::Last;
@@ -328,26 +331,32 @@ struct ColK {
         sizeof(double2) * (H + NTW + kLogTab) + (sizeof(unsigned) + sizeof(unsigned long long)) * kColRunsMax;
     static_assert(Radices<Rs...>::product == H, "plan");
     static_assert(T % 2 == 0, "threads cover whole row pairs");
+    static_assert(H % 2 == 0, "column plans: whole row pairs (the half-prefetch split)");
     // waves per SIMD of the launch bounds: sized for two resident blocks per
     // CU, one when the column and twiddles fill the LDS
     static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
     static constexpr int MINW = (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2;
-    // The prefetch form (PF, asked for by PFREQ): p per row gets an array of
-    // its own, so the column buffer is free once the last pass has read it,
-    // and the next column streams into it by LDS-DMA (no registers) during the
-    // epilogue -- where it fits beside as many blocks per CU as the plain form
-    // (3000 and 2000 rows: two; 6000: one).  4000 rows would drop to one
-    // block: plain form only.
+    // The next column streams into the column buffer by LDS-DMA (no
+    // registers) while the current one finishes (round 5).
+    //  * Full-prefetch form (PF): p per row gets an LDS array of its own, so
+    //    the whole buffer is free once the last pass has read it and the
+    //    whole next column is issued then -- where that fits beside as many
+    //    blocks per CU as without it (3000 and 2000 rows: two; 6000: one;
+    //    4000 rows would drop to one block and take the half form).
+    //  * Half-prefetch form: p stays in the lower half of the buffer; the
+    //    upper half streams in during the run walk, the lower half after
+    //    it, beside the atomics.  No LDS beyond the register-staged form's it
+    //    replaced (round 4), which measured slower in every configuration.
     static constexpr size_t lds_pf = lds_base + sizeof(double) * H;
-    static constexpr bool PF = PFREQ && lds_pf * BPC1 <= 160 * 1024;
+    static constexpr bool PF = FULL && lds_pf * BPC1 <= 160 * 1024;
     static constexpr size_t lds = PF ? lds_pf : lds_base;
 };
 
 // One column per block: blocks b, b^8, b^16, b^24 (one XCD) take the four
 // columns of the same 128-byte lines (two tiles), so each line is fetched once
-// into that XCD's L2 (the grid is a multiple of 32).  A step's tiles are
-// loaded at its start; the other blocks of the CU hide the latency (round 3:
-// prefetching the next column into registers measured slower, it cost VGPRs).
+// into that XCD's L2 (the grid is a multiple of 32).  The tiles of a step were
+// issued as LDS-DMA during the previous step (ColK's forms; prefetching into
+// registers measured slower in round 3: it cost VGPRs).
 // One 16-byte LDS-DMA per lane: global g -> LDS at the wave's base + lane x 16
 // (global_load_lds_dwordx4; M0 holds the wave-uniform LDS base).  Inline asm
 // rather than the builtin: the compiler would make every later LDS read wait
@@ -373,8 +382,8 @@ __device__ __forceinline__ void lds_dma16(const void* g, void* lds_wave_base) {
 // left alone): a DMA-filled buffer may be read after this and a barrier
 __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-template <int H, int T, bool PFREQ, int... Rs>
-__global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
+template <int H, int T, bool FULL, int... Rs>
+__global__ __launch_bounds__(T, (ColK<H, T, FULL, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
                                                      const unsigned* __restrict__ runs,
                                                      const uint8_t* __restrict__ segidx, int rstride,
                                                      unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
@@ -382,7 +391,7 @@ __global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct
                                                      const unsigned long long* __restrict__ sums0, int width,
                                                      double* __restrict__ dbg, double bscale, int ablate_arg,
                                                      int nimg, long istride, long bstride, long fstride, long sstride) {
-    using K = ColK<H, T, PFREQ, Rs...>;
+    using K = ColK<H, T, FULL, Rs...>;
     const int ablate = PHD_ABL(ablate_arg);
     using L = typename K::L;
     constexpr int R = K::R;
@@ -392,8 +401,8 @@ __global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct
     double2* lt = tw + K::NTW;                                 // log_mant's table
     unsigned long long* sl = reinterpret_cast<unsigned long long*>(lt + kLogTab);   // [kColRunsMax]
     unsigned* rl = reinterpret_cast<unsigned*>(sl + kColRunsMax);                   // [kColRunsMax]
-    // p per spectrum row: its own array in the prefetch form, else the
-    // column buffer (free once the last pass has read it)
+    // p per spectrum row: its own array in the full-prefetch form, else the
+    // lower half of the column buffer (free once the last pass has read it)
     double* lgb = K::PF ? reinterpret_cast<double*>(rl + kColRunsMax) : reinterpret_cast<double*>(buf);
     const int tid = threadIdx.x;
     // a batch: nimg images of one size, their intermediates, bin sums, max
@@ -428,13 +437,16 @@ __global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct
     const int prow0 = tid / 2, psub = 2 * half + (tid & 1);
     // the column of step u into the buffer by LDS-DMA (PF): element 2 prow0 +
     // (tid & 1) + c T is lane-linear, the wave's base + lane x 16 B
-    auto dma = [&](int u) {
+    // part 0: the whole column; 1: its upper half (buffer elements >= H / 2,
+    // free while p sits in the lower half), 2: the lower half
+    auto dma = [&](int u, int part) {
         const u32x4* src = reinterpret_cast<const u32x4*>(inter) + (size_t)prow0 * rs + (size_t)pair_at(u) * 4 + psub;
 #pragma unroll 1
         for (int c = 0; c < K::CR; c++) {
             const int pr = min(c * (T / 2), K::P - 1 - prow0);
             const int y = 2 * (prow0 + c * (T / 2)) + (psub & 1);
-            if (((2 * K::P) % T == 0 || tid + c * T < 2 * K::P) && (H % 2 == 0 || y < H))
+            if (((2 * K::P) % T == 0 || tid + c * T < 2 * K::P) && (H % 2 == 0 || y < H) &&
+                (part == 0 || (part == 1) == (tid + c * T >= H / 2)))
                 lds_dma16(src + (size_t)pr * rs, buf + (tid & ~63) + c * T);
         }
     };
@@ -453,29 +465,11 @@ __global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct
     sums = sums0 + im * sstride;
     double mx = 0.0;
     __syncthreads();
-    if (K::PF && u0 < un && !pf_late) dma(u0);
+    if (u0 < un && !pf_late) dma(u0, 0);
     for (int u = u0; u < un; u++) {
         const int kp = pair_at(u);
-        if (K::PF) {
-            if (pf_late) dma(u);
-            wait_vmem();                          // this wave's DMA of the column is in LDS
-        } else {
-            u32x4 pf[K::CR];
-            const u32x4* src = reinterpret_cast<const u32x4*>(inter) + (size_t)prow0 * rs + (size_t)kp * 4 + psub;
-#pragma unroll
-            for (int c = 0; c < K::CR; c++) {
-                // rows past the end re-read the last row pair (unused, no branch)
-                const int pr = min(c * (T / 2), K::P - 1 - prow0);
-                pf[c] = src[(size_t)pr * rs];
-            }
-            u32x4* dst = reinterpret_cast<u32x4*>(buf + 2 * prow0 + (psub & 1));
-#pragma unroll
-            for (int c = 0; c < K::CR; c++) {
-                const int y = 2 * (prow0 + c * (T / 2)) + (psub & 1);
-                if (((2 * K::P) % T == 0 || tid + c * T < 2 * K::P) && (H % 2 == 0 || y < H))
-                    dst[c * T] = pf[c];
-            }
-        }
+        if (pf_late) dma(u, 0);
+        wait_vmem();                              // this wave's DMA of the column is in LDS
         const int col = 2 * (2 * u + (quad >> 1)) + half;
         const bool live = col < wf;                       // the phantom column of an odd wf idles
         // the column's bin runs (image-independent, ~0.3 KB per column; ColRuns)
@@ -513,10 +507,11 @@ __global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct
             L::load(buf, v, tid);
             L::compute(v, tw + K::PL::last_tw_offset, tid);
         }
-        // PF: nothing waits for the buffer after the last pass's reads, so p, the
-        // run list and the barrier come first and the next column's DMA is
-        // issued behind them (the walk and the atomics run while it lands);
-        // plain: the barrier first, p then overwrites the buffer
+        // Full form: nothing waits for the buffer after the last pass's reads, so
+        // p, the run list and the barrier come first and the whole next column
+        // is issued behind them (the walk and the atomics run while it lands).
+        // Half form: a barrier first (p then overwrites the lower half), the
+        // upper half issued behind the next barrier, the lower after the walk.
         if (!K::PF) __syncthreads();               // every thread has read its last-pass inputs
         // lgb: p per spectrum row, 1 for p < 1 (log 0)
 #pragma unroll
@@ -538,13 +533,14 @@ __global__ __launch_bounds__(T, (ColK<H, T, PFREQ, Rs...>::MINW)) void k_cols_ct
             if (tid + k * T < kColRunsMax) rl[tid + k * T] = rreg[k];
         // PF: the run loads (and any debug stores) retire before a DMA is in
         // flight, so no later wait of the compiler's counts the DMA
-        if (K::PF) wait_vmem();
+        wait_vmem();
         __syncthreads();
-        if (K::PF && u + 1 < un && !pf_late) dma(u + 1);
+        if (u + 1 < un && !pf_late) dma(u + 1, K::PF ? 0 : 1);
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
         if (!(ablate & 2)) walk_runs<K::E>(lgb, tid * K::E, H, rl, sidx, sl, bscale, lt);
         __syncthreads();
+        if (!K::PF && u + 1 < un && !pf_late) dma(u + 1, 2);   // p is read: the lower half too
         // the column's run sums into the image's bins (a bin met by two runs of
         // a column gets two atomics); entries past the sentinel start at H
         if (!(ablate & 8)) {
@@ -634,7 +630,8 @@ hipError_t cols_ct_form(const double2* inter, int width, int wf, const ColBins& 
     return hipGetLastError();
 }
 
-// pf: the prefetch form where the plan has one (FftSel::col_pf)
+// pf: the full-prefetch form where the plan has one (FftSel::col_pf), else
+// the half-prefetch form
 template <int H, int T, int... Rs>
 hipError_t cols_ct(const double2* inter, int width, int wf, const ColBins& cb, unsigned long long* bin_sums,
                    double* fmax_part, const double2* tw, const unsigned long long* sums, double* dbg,

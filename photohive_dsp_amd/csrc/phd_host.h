@@ -283,11 +283,12 @@ struct FftSel {
     const double2* tw_c = nullptr;
     int col_blocks = 0;   // entries of the per-block max partials
     ColBins cbins;        // compile-time column pass: its per-column polar-bin runs
-    // compile-time column pass: its prefetch form (the next column streams into
-    // LDS during the epilogue) where the plan has one; run_reports turns it off
-    // when another lane's two-block K1 shares the CUs (measured)
+    // compile-time column pass: its full-prefetch form (the whole next column
+    // streams into LDS during the epilogue) where the plan has one, else the
+    // half-prefetch form; run_reports takes the half form when another lane's
+    // two-block K1 shares the CUs (measured)
     bool col_pf = true;
-    // phd_debug_column_form: -1 the library's choice, 0 plain, 1 prefetch form
+    // phd_debug_column_form: -1 the library's choice, 0 half-prefetch, 1 full
     static int forced_form();
     // the generic path (a side above the LDS limit or with a large prime
     // factor): row pairs -> global row transforms -> split / transpose, then

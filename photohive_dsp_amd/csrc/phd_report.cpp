@@ -489,11 +489,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (!select_fft(c, height, width, nbins, d_imgs, n, &fs, tbl, ct_batchable)) return false;
     const Context::Cls* cls = get_cls(c, gp);
     if (!cls) return false;
-    // the column pass's prefetch form: on a call split over two lanes whose K1
-    // runs the two-block form (one 512-thread block per CU beside the other
-    // lane's FFTs) it measured 3 % slower (8.67k against 8.95k images/s at
-    // 4000x3000, 18/2/3), where FFT-only calls and the fine grids' one-block
-    // K1 gain 3 %
+    // the column pass's full-prefetch form (24 KB more LDS per block): on a
+    // call split over two lanes whose K1 runs the two-block form (one
+    // 512-thread block per CU beside the other lane's FFTs) the half-prefetch
+    // form measured 9.05k images/s against its 8.67k at 4000x3000, 18/2/3,
+    // where FFT-only calls and the fine grids' one-block K1 gain with the full
+    // form
     if (FftSel::forced_form() < 0 && ds <= 1 && k1_blocks_per_cu() == 1 && cls->fc.k1t_cshift2 >= 0)
         fs.col_pf = false;
 

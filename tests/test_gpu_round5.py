@@ -2,7 +2,7 @@
 process (the bench's default configuration), the compile-time size whose
 polar-bin table has too many runs per column for the column pass's run lists
 (the runtime-plan fallback) against the oracle, and the column pass's two
-forms (plain and LDS-DMA prefetch) against each other."""
+forms (half- and full-prefetch by LDS-DMA) against each other."""
 import ctypes
 import json
 import os
@@ -55,7 +55,7 @@ def test_column_runs_fallback_4000x3000_against_oracle():
         assert_report_matches(rep, g)
 
 
-# (height, width): every compile-time column plan with a prefetch form, each
+# (height, width): every compile-time column plan with a full-prefetch form, each
 # with a compile-time row plan for its width
 PF_SIZES = [(3000, 4000), (2000, 3000), (6000, 4000), (1536, 2048), (1080, 1920), (1280, 720),
             (720, 1280), (640, 480), (480, 640), (512, 512)]
@@ -63,7 +63,7 @@ PF_SIZES = [(3000, 4000), (2000, 3000), (6000, 4000), (1536, 2048), (1080, 1920)
 
 @pytest.mark.parametrize("h,w", PF_SIZES)
 def test_column_forms_bit_identical(h, w):
-    """The compile-time column pass's plain form and its LDS-DMA prefetch form
+    """The compile-time column pass's half- and full-prefetch forms
     (phd_debug_column_form) give the same bins, max and blur vectors for a
     batch (the polar bins are fixed-point sums: bit-identical whatever the
     order), on one lane and, at the default lanes, for a split batch."""
@@ -78,12 +78,12 @@ def test_column_forms_bit_identical(h, w):
         assert rc == 0
     prev = L.lib.phd_debug_column_form(0)
     try:
-        plain = phd.report_device(t)
+        half = phd.report_device(t)
         assert L.lib.phd_debug_column_form(1) == 0
         pf = phd.report_device(t)
     finally:
         L.lib.phd_debug_column_form(prev)
-    for a, b in zip(plain, pf):
+    for a, b in zip(half, pf):
         assert np.array_equal(np.array(a.blur_profile.bins), np.array(b.blur_profile.bins))
         assert [(v.angle, v.magnitude) for v in a.blur_vectors] == [(v.angle, v.magnitude) for v in b.blur_vectors]
         assert a.color_palette.group_ids == b.color_palette.group_ids
