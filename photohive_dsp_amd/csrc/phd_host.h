@@ -260,7 +260,7 @@ private:
     std::thread th_;
 };
 LaneWorker* lane_worker();
-// lanes a large device batch is split over (PHD_LANES, default 1; phd_set_lanes)
+// lanes a large device batch is split over (PHD_LANES, default 2; phd_set_lanes)
 int lanes_setting();
 // The stream a call works on: the caller's, or (NULL) the library's own stream
 // ordered after every prior operation of the legacy null stream, so device

@@ -1222,35 +1222,22 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
     return 0;
 }
 
-// The FFT + blur-profile path alone (BASELINE config 4): the row and column
-// passes per image, the channel sums of remove_dc_bias from the row pass
-// (compile-time plans) or the statistics pass (others), one read-back.
-extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
-                                     size_t image_stride, const phd_config* cfg, double* bins_out,
-                                     Blur_Vector* vectors_out, void* stream) {
-    clear_error();
-    if (!d_rgb || !cfg || !bins_out || !vectors_out || n_images <= 0) {
-        set_error("phd_blur_batch_device: bad arguments");
-        return -1;
-    }
-    std::string why;
-    if (!validate_config(*cfg, &why)) {
-        set_error(why);
-        return -1;
-    }
-    if (!precheck(height, width)) return -1;
-    Context* c = get_context();
-    if (!c) return -1;
-    std::lock_guard<std::mutex> lk(c->mu);
+// The FFT + blur-profile path alone (BASELINE config 4) over n same-size
+// device images on one context (its lock held by the caller): the row and
+// column passes per image on the context's stream, the channel sums of
+// remove_dc_bias from the row pass (compile-time plans) or the statistics pass
+// (others), one read-back.  `lanes`: the lanes the whole call is split over.
+static int blur_run(Context* c, int lanes, const uint8_t* const* imgs, int n_images, int height, int width,
+                    const phd_config* cfg, double* bins_out, Blur_Vector* vectors_out, void* stream) {
     const hipStream_t st = work_stream(c, stream);
-    const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
-    std::vector<const uint8_t*> imgs(n_images);
-    for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
     const int nbins = cfg->radius_partitions * cfg->angle_partitions, wf = width / 2 + 1;
     const BlurTable* tbl = get_table(c, height, width, cfg->radius_partitions, cfg->angle_partitions);
     if (!tbl) return -1;
     FftSel fs;
-    if (!select_fft(c, height, width, nbins, imgs.data(), n_images, &fs, tbl)) return -1;
+    if (!select_fft(c, height, width, nbins, imgs, n_images, &fs, tbl)) return -1;
+    // the half-prefetch column form when the other lane's column passes share
+    // the CUs (13.12k vs 13.0k images/s at config 4)
+    if (FftSel::forced_form() < 0 && lanes >= 2) fs.col_pf = false;
     // per image: bins, max partials, channel sums (+ the statistics pass's chunk slots)
     const long npix = (long)height * width;
     const int nchunks = (int)((npix + kChunk - 1) / kChunk);
@@ -1320,6 +1307,40 @@ extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int hei
                     vectors_out + (size_t)i * 10);
     }
     return 0;
+}
+
+extern "C" int phd_blur_batch_device(const uint8_t* d_rgb, int n_images, int height, int width,
+                                     size_t image_stride, const phd_config* cfg, double* bins_out,
+                                     Blur_Vector* vectors_out, void* stream) {
+    clear_error();
+    if (!d_rgb || !cfg || !bins_out || !vectors_out || n_images <= 0) {
+        set_error("phd_blur_batch_device: bad arguments");
+        return -1;
+    }
+    std::string why;
+    if (!validate_config(*cfg, &why)) {
+        set_error(why);
+        return -1;
+    }
+    if (!precheck(height, width)) return -1;
+    Context* c = get_context();
+    if (!c) return -1;
+    const size_t stride = image_stride ? image_stride : 3 * (size_t)width * height;
+    std::vector<const uint8_t*> imgs(n_images);
+    for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
+    const int nbins = cfg->radius_partitions * cfg->angle_partitions;
+    // two lanes for large batches on the library's streams, as the full
+    // report's batches: the second half on lane 1 (its own context, stream
+    // and intermediate), each lane's launch gaps and kernel tails under the
+    // other's kernels
+    int rc[2] = {0, 0};
+    on_lanes(c, n_images >= 16 && !stream, [&](Context* cl, int lane, int nl) {
+        const int h = nl == 2 ? n_images / 2 : n_images;
+        const int i0 = lane ? h : 0, m = lane ? n_images - h : h;
+        rc[lane] = blur_run(cl, nl, imgs.data() + i0, m, height, width, cfg, bins_out + (size_t)i0 * nbins,
+                            vectors_out + (size_t)i0 * 10, stream);
+    });
+    return rc[0] < 0 || rc[1] < 0 ? -1 : 0;
 }
 
 constexpr long kMixedGroupMax = 1024;                         // images per run, any size

@@ -87,3 +87,26 @@ def test_column_forms_bit_identical(h, w):
         assert np.array_equal(np.array(a.blur_profile.bins), np.array(b.blur_profile.bins))
         assert [(v.angle, v.magnitude) for v in a.blur_vectors] == [(v.angle, v.magnitude) for v in b.blur_vectors]
         assert a.color_palette.group_ids == b.color_palette.group_ids
+
+
+@pytest.mark.parametrize("kind,h,w", [("structured", 600, 800), ("motion", 401, 577)])
+def test_blur_batch_two_lanes_match_one_lane(kind, h, w):
+    """phd_blur_batch_device (config 4) splits a batch of >= 16 images over the
+    two library lanes like the full report's batches: 20 images (a
+    compile-time size and a runtime-plan size) give the one-lane call's bins
+    (fp64 atomics in any order: 1e-12) and vectors, on two calls in a row."""
+    phd, L, torch = _phd()
+    from photohive_dsp_amd import synth
+    from photohive_dsp_amd.core import blur_profiles_device
+    imgs = np.stack([synth.make(kind, h, w, 900 + i) for i in range(20)])
+    t = torch.from_numpy(imgs).cuda()
+    prev = L.lib.phd_set_lanes(1)
+    try:
+        b1, v1 = blur_profiles_device(t)
+        L.lib.phd_set_lanes(2)
+        runs = [blur_profiles_device(t) for _ in range(2)]
+    finally:
+        L.lib.phd_set_lanes(prev)
+    for b2, v2 in runs:
+        np.testing.assert_allclose(b2, b1, rtol=1e-12, atol=1e-15)
+        assert v2 == v1
