@@ -285,7 +285,10 @@ int phd_profile_read(int kernel, double* total_ms, long* launches);
  * (1 or 2; default 2, or PHD_LANES).  Each lane is an independent context with
  * its own streams and workspaces; the second runs on a library thread, so the
  * two halves' kernels, host phases and launch gaps overlap (+10-13 % images/s
- * at 4000x3000 over one lane, bench.py's one_lane object).  Results do not
+ * at 4000x3000 over one lane, bench.py's one_lane object).  It applies to
+ * phd_report_batch_device, phd_blur_batch_device (the second half of the
+ * batch on lane 1) and phd_report_batch_device_mixed (size groups to the
+ * lanes in turn).  Results do not
  * depend on it.  With
  * two lanes, phd_last_timings and PHD_VERBOSE's stage lines cover lane 0's half
  * of a batch only (the stage timings are per calling thread).  lanes < 1 only
