@@ -89,16 +89,17 @@ def test_column_forms_bit_identical(h, w):
         assert a.color_palette.group_ids == b.color_palette.group_ids
 
 
-@pytest.mark.parametrize("kind,h,w", [("structured", 600, 800), ("motion", 401, 577)])
-def test_blur_batch_two_lanes_match_one_lane(kind, h, w):
+@pytest.mark.parametrize("kind,h,w,n", [("structured", 600, 800, 20), ("motion", 401, 577, 17)])
+def test_blur_batch_two_lanes_match_one_lane(kind, h, w, n):
     """phd_blur_batch_device (config 4) splits a batch of >= 16 images over the
-    two library lanes like the full report's batches: 20 images (a
-    compile-time size and a runtime-plan size) give the one-lane call's bins
-    (fp64 atomics in any order: 1e-12) and vectors, on two calls in a row."""
+    two library lanes like the full report's batches: 20 and 17 images (a
+    compile-time size and a runtime-plan size; halves of 10 / 10 and 8 / 9)
+    give the one-lane call's bins (fp64 atomics in any order: 1e-12) and
+    vectors, on two calls in a row."""
     phd, L, torch = _phd()
     from photohive_dsp_amd import synth
     from photohive_dsp_amd.core import blur_profiles_device
-    imgs = np.stack([synth.make(kind, h, w, 900 + i) for i in range(20)])
+    imgs = np.stack([synth.make(kind, h, w, 900 + i) for i in range(n)])
     t = torch.from_numpy(imgs).cuda()
     prev = L.lib.phd_set_lanes(1)
     try:
