@@ -506,8 +506,6 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     // of 1 / 2 / 4 / 8 give FFT stages of 0.857 / 0.838 / 0.828 / 0.823 ms and
     // 6.16k / 6.21k / 6.17k / 6.08k images/s.
     static const int dl_group = phd_knob("PHD_DL_GROUP") ? std::max(1, atoi(phd_knob("PHD_DL_GROUP"))) : 2;
-    auto dl_end = [&](int i) { return (i + 1) % dl_group == 0 || i == n - 1; };
-    auto dl_last = [&](int i) { return std::min(n - 1, (i / dl_group + 1) * dl_group - 1); };
     // fused palette (one pixel pass): ds == 1 and the fused K1's LDS fits; else K1 + K3
     const bool fused = ds <= 1 && fused_palette_ok(gp);
     const Layout L = make_layout(n, gp.tl, nchunks, nbins, ncrops, ncolblocks, fused ? HueCells::count(gp) : 0);
@@ -525,6 +523,12 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     if (gbatch) Q = std::max(1, std::min(n, (int)(((size_t)128 << 20) / inter_one)));
     const bool ctbatch = fs.ct && ct_batchable && L.a_bytes % 8 == 0 && L.c_bytes % 8 == 0;
     if (ctbatch) Q = q_ct;
+    // batched FFT launches finish a whole group of Q images at once: one
+    // event, one download and one host wait per group (small images were
+    // bound by ~3 HIP calls and a wait per pair of images: DESIGN.md section 12)
+    const int dlg = gbatch || ctbatch ? Q : dl_group;
+    auto dl_end = [&](int i) { return (i + 1) % dlg == 0 || i == n - 1; };
+    auto dl_last = [&](int i) { return std::min(n - 1, (i / dlg + 1) * dlg - 1); };
     if (!ensure_device(&c->d_ws, &c->ws_bytes, L.dev_total) || !ensure_pinned(c, L.pin_total) ||
         !ensure_device((void**)&c->d_inter, &c->inter_bytes, (size_t)Q * inter_one))
         return false;
