@@ -828,14 +828,13 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
     const auto t_dec = std::chrono::steady_clock::now();
     auto t_sync = t_dec;
 
-    int failures = 0;
-    for (int i = 0; i < n; i++) {
-        if (i == 0 || dl_end(i - 1)) PHD_HIP(hipEventSynchronize(c->ev_img_dl[dl_last(i)]));
-        if (i == n - 1) t_sync = std::chrono::steady_clock::now();
-        if (!ok[i]) {
-            failures++;
-            continue;
-        }
+    // each download group's reports are assembled once its copy is done; a
+    // group of 8 or more (batched FFT groups of small images, ~10 us per
+    // report at 36/4/5) on the host pool
+    std::vector<std::string>& asm_why = fail_why;             // the decisions' messages are set already
+    auto assemble_one = [&](int i) {
+        if (!ok[i]) return;
+        asm_why[i].clear();
         const uint8_t* a = hp + L.A(i);
         const uint8_t* cc = hc + (size_t)i * L.c_bytes;
         const unsigned long long* sums = (const unsigned long long*)(a + L.a_sums);
@@ -852,16 +851,23 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
             for (size_t k = 0; k < hsum[i].size(); k++) hsum[i][k] += pal[k];
             pal = hsum[i].data();
         }
-        std::string w;
         out[i] = assemble(st_i, s_acc / (double)n_hsv, dec[i], pal, n_hsv, *tbl,
                           (const unsigned long long*)(cc + L.c_bins), fmax, cfg, crops,
-                          (const double*)(cc + L.c_sharp), &w);
-        if (!out[i]) {
-            set_error(w);
-            failures++;
-        } else {
-            status[i] = 0;
-        }
+                          (const double*)(cc + L.c_sharp), &asm_why[i]);
+        if (out[i]) status[i] = 0;
+    };
+    for (int i0 = 0; i0 < n; i0 = dl_last(i0) + 1) {
+        const int i1 = dl_last(i0), m = i1 - i0 + 1;
+        PHD_HIP(hipEventSynchronize(c->ev_img_dl[i1]));
+        if (i1 == n - 1) t_sync = std::chrono::steady_clock::now();
+        if (m >= 8 && pool->size() > 0) pool->parallel_for(m, [&](int k) { assemble_one(i0 + k); });
+        else
+            for (int i = i0; i <= i1; i++) assemble_one(i);
+    }
+    int failures = 0;
+    for (int i = 0; i < n; i++) {
+        if (ok[i] && !out[i]) set_error(asm_why[i]);          // on this thread (thread-local message)
+        failures += !out[i];
     }
     const auto t_end = std::chrono::steady_clock::now();
     PHD_HIP(hipEventSynchronize(c->ev[4]));
@@ -870,8 +876,9 @@ bool run_reports(Context* c, const uint8_t* const* d_imgs, int n, int height, in
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
     // device stages, then host: total, enqueue, decisions + pass-2 enqueue, assembly
-    // (a per-image D2H + assembly pipeline and a host thread pool were both
-    // measured slower: extra stream joins, thread wake-up latency)
+    // (a per-image D2H + assembly pipeline was measured slower: extra stream
+    // joins; the host pool assembles only groups of 8 or more, where its
+    // wake-up latency is paid once per group)
     double tm[8] = {ms_between(c->ev[0], c->ev[1]), ms_between(c->ev[1], c->ev[2]),
                     ms_between(c->ev[2], c->ev[3]), ms_between(c->ev[0], c->ev[4]), ms(t_host0, t_end),
                     ms(t_host0, t_enq), ms(t_k1, t_dec), ms(t_sync, t_end)};
