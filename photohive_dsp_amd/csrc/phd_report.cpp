@@ -1152,9 +1152,12 @@ extern "C" int phd_report_batch_device(const uint8_t* d_rgb, int n_images, int h
     for (int i = 0; i < n_images; i++) imgs[i] = d_rgb + (size_t)i * stride;
     // two lanes for large batches on the library's streams: the second half on
     // lane 1, so each half's host phases and launch gaps overlap the other's
-    // kernels
+    // kernels.  Lane 0 takes 51.2 % (262 of 512): with equal halves lane 1
+    // finished ~1.6 ms after lane 0 per 512-image call at 4000x3000, and the
+    // call took 56.2 ms against 55.8-55.9 with 262 / 250 (56.0-56.3 with 268 /
+    // 244; profiles/r05/lane_split_ab.log)
     on_lanes(c, n_images >= 16 && !stream, [&](Context* cl, int lane, int nl) {
-        const int h = nl == 2 ? n_images / 2 : n_images;
+        const int h = nl == 2 ? (int)(((long)n_images * 131 + 128) / 256) : n_images;
         const int i0 = lane ? h : 0, m = lane ? n_images - h : h;
         run_reports(cl, imgs.data() + i0, m, height, width, *cfg, nullptr, out + i0, status + i0,
                     (hipStream_t)stream);
