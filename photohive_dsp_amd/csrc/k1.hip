@@ -258,6 +258,10 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
     Mom m{0, 0, 0, 0, 0, 0};
     int seg_c0 = c;
     long seg_it0 = it0;
+    // the next chunk's first 4-pixel group, loaded before the fold of the
+    // current one (its HBM latency then passes under the fold's barriers)
+    unsigned p0 = 0, p1 = 0, p2 = 0;
+    bool have_pf = false, p_ok = false;                         // (have_pf block-uniform)
     for (long it = it0; it < it1; it++) {
         const long base = (long)c * kChunk;
         const int cimg = img, cc = c;
@@ -284,8 +288,9 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                 x1 = ok ? l1 : 0u;
                 x2 = ok ? l2 : 0u;
             };
-            unsigned a0, a1, a2;
-            ld(0, a0, a1, a2);
+            // (the prefetch's mask applied here, so nothing waits for it before the fold)
+            unsigned a0 = p_ok ? p0 : 0u, a1 = p_ok ? p1 : 0u, a2 = p_ok ? p2 : 0u;
+            if (!have_pf) ld(0, a0, a1, a2);
             CellRun run{-1, 0u, 0u, 0.0, 0.0};
             unsigned same0 = 0;
             auto loop = [&](auto mg) __attribute__((always_inline)) {
@@ -374,6 +379,17 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         if (pad > 0 && tid == 0)
             atomicAdd(reinterpret_cast<unsigned long long*>(cells + kCellBytes * (zcell << cshift)),
                       (unsigned long long)(-pad));
+        {
+            // (c, img) are the next chunk's already; as ld(0) of that chunk
+            // (unconditional: a load under a branch is waited for at the join)
+            have_pf = more;
+            const long nbase = (long)c * kChunk;
+            p_ok = more && (nbase + kChunk <= full_end || nbase + 4L * tid < full_end);
+            gu32t* q = (gu32t*)((more ? imgs[img] : cip) + (p_ok ? (unsigned)(3 * (nbase + 4L * tid)) : 0u));
+            p0 = q[0];
+            p1 = q[1];
+            p2 = q[2];
+        }
         __syncthreads();
         merge = 5 * vote[16 * vpar] > (unsigned)kT;              // the next chunk's mode
         // fold the chunk's count words: one thread per cell sums its C copies;
