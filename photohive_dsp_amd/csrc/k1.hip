@@ -278,15 +278,24 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             // took 128 and spilled; the other waves of the CU hide the loads
             // (groups past the image end read pixel 0, masked below)
             const bool full = base + kChunk <= full_end;          // block-uniform: no group past the end
-            auto ld = [&](int st, unsigned& x0, unsigned& x1, unsigned& x2) {
-                // always a valid address, so the loads are unconditional (a
-                // guarded load became an exec-masked branch per word)
+            // always a valid address, so the loads are unconditional (a
+            // guarded load became an exec-masked branch per word); the words
+            // of a group past the image end are masked where they are used
+            // (a load whose value is selected at once, or that sits under a
+            // branch, is waited for right there)
+            auto ld_raw = [&](int st, unsigned& x0, unsigned& x1, unsigned& x2) {
                 const bool ok = full || base + 4L * tid + 4L * kT * st < full_end;
                 gu32t* q = (gu32t*)(cip + (ok ? (unsigned)(3 * (base + 4L * tid)) + 12u * kT * st : 0u));
-                const unsigned l0 = q[0], l1 = q[1], l2 = q[2];
-                x0 = ok ? l0 : 0u;
-                x1 = ok ? l1 : 0u;
-                x2 = ok ? l2 : 0u;
+                x0 = q[0];
+                x1 = q[1];
+                x2 = q[2];
+                return ok;
+            };
+            auto ld = [&](int st, unsigned& x0, unsigned& x1, unsigned& x2) {
+                const bool ok = ld_raw(st, x0, x1, x2);
+                x0 = ok ? x0 : 0u;
+                x1 = ok ? x1 : 0u;
+                x2 = ok ? x2 : 0u;
             };
             // (the prefetch's mask applied here, so nothing waits for it before the fold)
             unsigned a0 = p_ok ? p0 : 0u, a1 = p_ok ? p1 : 0u, a2 = p_ok ? p2 : 0u;
@@ -297,14 +306,15 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                 constexpr bool M = decltype(mg)::value;
 #pragma unroll 1
                 for (int st = 0; st < kG; st++) {
-                    unsigned n0 = 0, n1 = 0, n2 = 0;
-                    if (st + 1 < kG) ld(st + 1, n0, n1, n2);
+                    // the next group (the last step reloads its own: unused)
+                    unsigned n0, n1, n2;
+                    const bool nok = ld_raw(st + 1 < kG ? st + 1 : st, n0, n1, n2);
                     emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, cells, cshift, copy, G, &run,
                                                      st == 0 ? &same0 : nullptr)
                              << (4 * st);
-                    a0 = n0;
-                    a1 = n1;
-                    a2 = n2;
+                    a0 = nok ? n0 : 0u;
+                    a1 = nok ? n1 : 0u;
+                    a2 = nok ? n2 : 0u;
                 }
                 if (M && run.cell >= 0) {
                     K1Px q;
