@@ -1038,9 +1038,12 @@ __global__ __launch_bounds__(kPartThreads) void k_partial_sums_img(
         bool ok[4];
         unsigned hv;
     };
+    // (unconditional loads, lanes >= ne reading entry ne - 1's count: a load
+    // whose value is selected at once, or that sits under a branch, is
+    // waited for right there; process() tests lane < ne)
     auto fetch = [&](long u, Unit& x) {
         const long ub = u * kUnit;
-        x.hv = lane < ne ? chunk_hist[(ub / kChunk) * tl + egrp[lane]] : 0u;
+        x.hv = chunk_hist[(ub / kChunk) * tl + egrp[lane < ne ? lane : ne - 1]];
 #pragma unroll
         for (int st = 0; st < 4; st++) {
             const long p0 = ub + 4L * tid + 4L * kPartThreads * st;
@@ -1096,18 +1099,16 @@ __global__ __launch_bounds__(kPartThreads) void k_partial_sums_img(
     };
     // two units in flight: the next one's loads are issued before this one's
     // classification (the walk is otherwise bound by the load latency)
-    Unit ua, ub2;
+    // (a unit past the walk's end is fetched as its last unit, and not used)
     const long gy = gridDim.y;
-    long u = blockIdx.y;
-    if (u <= umax) fetch(u, ua);
-    while (u <= umax) {
-        const long v = u + gy;
-        if (v <= umax) fetch(v, ub2);
-        process(u, ua);
-        if (v > umax) break;
-        u = v + gy;
-        if (u <= umax) fetch(u, ua);
-        process(v, ub2);
+    Unit cur;
+    if ((long)blockIdx.y <= umax) fetch(blockIdx.y, cur);
+#pragma unroll 1
+    for (long u = blockIdx.y; u <= umax; u += gy) {
+        Unit nxt;
+        fetch(u + gy <= umax ? u + gy : umax, nxt);
+        process(u, cur);
+        cur = nxt;
     }
     if (blockIdx.y == 0)
         for (int e = tid; e < ne; e += kPartThreads) {
