@@ -16,6 +16,8 @@ from photohive_dsp_amd.structures import Full_Report_Data  # noqa: E402
 import torch  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+if os.environ.get("COLUMN_FORM"):                 # 0 half / 1 full prefetch form (phd_debug_column_form)
+    lib.phd_debug_column_form(int(os.environ["COLUMN_FORM"]))
 B, H, W = 512, 3000, 4000
 nb = H * W * 3
 t = torch.empty(B * nb, dtype=torch.uint8, device="cuda")
