@@ -53,8 +53,8 @@ def parse(argv=None):
                         "lane, where each launch of the dominant kernel runs alone and its events price it")
     p.add_argument("--hw-queues", type=int, default=8,
                    help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises; 0 keeps the environment's, "
-                        "where the package's own default is 8): two lanes drive 4 HIP streams beside HIP's copy "
-                        "traffic (round 5: 8.60-8.77k images/s with HIP's 4 queues, 8.87-8.97k with 8)")
+                        "HIP's own default is 4): two lanes drive 4 HIP streams beside HIP's copy traffic (round 5: "
+                        "8.60-8.77k images/s with HIP's 4 queues, 8.87-8.97k with 8)")
     p.add_argument("--no-one-lane", action="store_true",
                    help="skip the one-lane repeat of the headline (one_lane)")
     p.add_argument("--height", type=int, default=3000)
@@ -71,6 +71,9 @@ def parse(argv=None):
     p.add_argument("--config5-images", type=int, default=4096, help="config 5 total images (all ranks)")
     p.add_argument("--plan-only", action="store_true",
                    help="no GPU: start the ranks, shard configs 2/4/5 and merge the counters (gloo), print the plan")
+    p.add_argument("--plan-visible-devices", type=int, default=None,
+                   help="--plan-only: devices the ranks would see (default: torch.cuda.device_count(); 1 rehearses "
+                        "several ranks on one card, which the line then reports as n_gpus 1)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                    help="per-kernel PMC traffic summary written by tools/pmc_collect.py")
     return p.parse_args(argv)
@@ -374,10 +377,11 @@ def pipeline_headline_roofline(value, hl, args):
 class Ctx:
     """Per-rank state shared by the configs."""
 
-    def __init__(self, args, world, rank, backend):
+    def __init__(self, args, world, rank, backend, dev=None):
         import torch
         from photohive_dsp_amd.lib import last_error, lib
         self.args, self.world, self.rank, self.backend = args, world, rank, backend
+        self.dev = dev            # this rank's device index (n_gpus = distinct devices over the ranks)
         self.torch, self.lib, self.last_error = torch, lib, last_error
 
     def barrier(self):
@@ -388,7 +392,7 @@ class Ctx:
     def merge(self, elapsed, images, pixels, alg_bytes, kernel_ms=0.0, launches=0.0):
         from photohive_dsp_amd.shard import merge_counters
         return merge_counters([elapsed, images, pixels, alg_bytes, kernel_ms, launches],
-                              device="cuda" if self.backend == "nccl" else "cpu")
+                              device="cuda" if self.backend == "nccl" else "cpu", dev_index=self.dev)
 
     def fill(self, t, seed):
         assert self.lib.phd_fill_uniform_device(t.data_ptr(), t.numel(), seed, None) == 0, self.last_error()
@@ -746,7 +750,8 @@ def config4(cx, total, h=3000, w=4000, iters=3):
     ab = float(algorithmic_bytes("fft_cols", h, w))
     return {"workload": f"{total} x {h}x{w} RGB8 over {cx.world} GPU, FFT + blur_profile only, device-resident, "
                         f"{lanes} library lane(s)",
-            "scaling": "strong", "n_gpus": cx.world, "images_per_gpu_max": int(np.ceil(total / cx.world)),
+            "scaling": "strong", "n_gpus": m["devices"], "ranks": cx.world,
+            "images_per_gpu_max": int(np.ceil(total / cx.world)),
             "images_per_s": round(m["images"] / m["elapsed"], 1),
             "ms_per_pass_wall": round(1000 * m["elapsed"], 3),
             "hbm_GB_per_s_path": round(m["alg_bytes"] / m["elapsed"] / 1e9, 1),
@@ -801,7 +806,7 @@ def config5(cx, total, iters=4):
     return {"workload": f"{total} mixed-size RGB8 images (seed 5, {len(set(sizes_all))} sizes, "
                         f"{sum(h * w for h, w in sizes_all) / 1e6:.0f} Mpx) over {cx.world} GPU (LPT by pixels), "
                         f"full report, h/s/v 36/4/5, device-resident, {cx.lib.phd_set_lanes(0)} library lane(s)",
-            "scaling": "strong", "n_gpus": cx.world,
+            "scaling": "strong", "n_gpus": m["devices"], "ranks": cx.world,
             "images_per_s": round(m["images"] / m["elapsed"], 1),
             "megapixels_per_s": round(m["pixels"] / m["elapsed"] / 1e6, 1),
             "hbm_GB_per_s_algorithmic": round(m["alg_bytes"] / m["elapsed"] / 1e9, 1),
@@ -820,16 +825,21 @@ def plan_only(args, world, rank):
     c4 = shard.assign([(H, W)] * args.config4_images, world)[rank]
     sizes5 = shard.mixed_sizes(args.config5_images, 5)
     c5 = shard.assign(sizes5, world)[rank]
+    visible = args.plan_visible_devices
+    if visible is None:
+        import torch
+        visible = torch.cuda.device_count()        # counts without initialising HIP
+    dev = shard.device_of(int(os.environ.get("LOCAL_RANK", rank)), visible)
     out = {}
     for name, n, pix, ab in (("config2", B, B * H * W, B * algorithmic_bytes("report", H, W)),
                              ("config4", len(c4), len(c4) * H * W, len(c4) * algorithmic_bytes("blur_path", H, W)),
                              ("config5", len(c5), sum(sizes5[i][0] * sizes5[i][1] for i in c5),
                               sum(algorithmic_bytes("report", *sizes5[i]) for i in c5))):
-        m = shard.merge_counters([1.0 + rank, n, pix, ab])
+        m = shard.merge_counters([1.0 + rank, n, pix, ab], dev_index=dev)
         out[name] = {"images": int(m["images"]), "pixels": int(m["pixels"]), "alg_bytes": int(m["alg_bytes"]),
                      "elapsed_max": m["elapsed"]}
     if rank == 0:
-        print(json.dumps({"plan_only": True, "n_gpus": world, **out}), flush=True)
+        print(json.dumps({"plan_only": True, "n_gpus": m["devices"], "ranks": world, **out}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
@@ -868,12 +878,12 @@ def main(argv=None):
         if args.cpu_procs:
             topo["procs_reason"] = f"--cpu-procs {args.cpu_procs}"
         cpu = cpu_baseline(args.height, args.width, topo, procs)
-    # the package before torch: it sets GPU_MAX_HW_QUEUES (when unset) ahead of
-    # HIP's initialisation (--hw-queues 0 then runs on the package's default)
+    # the package before torch (its lib.py binds torch's HIP runtime file first)
     import photohive_dsp_amd  # noqa: F401
     import torch
+    from photohive_dsp_amd import shard
     ndev = torch.cuda.device_count()
-    dev = local % ndev if ndev else local
+    dev = shard.device_of(local, ndev)
     torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
@@ -881,7 +891,7 @@ def main(argv=None):
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-    cx = Ctx(args, world, rank, backend)
+    cx = Ctx(args, world, rank, backend, dev)
     dump_maps("ctx")
 
     cx.lib.phd_set_lanes(args.lanes)                  # every config of this run
@@ -934,7 +944,8 @@ def main(argv=None):
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "images/s",
-            "n_gpus": world,
+            "n_gpus": m["devices"],
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000 * m["elapsed"] / args.steps, 3),
@@ -946,7 +957,7 @@ def main(argv=None):
             "config": {"workload": f"full report, {H}x{W} RGB8, batch {B}/GPU, {hl['lanes']} library lane(s), "
                                    "device-resident",
                        "global_batch": B * world, "image": f"{H}x{W}",
-                       "parallelism": f"images sharded over {world} GPU"},
+                       "parallelism": f"images sharded over {world} rank(s) on {m['devices']} GPU"},
             "hbm_GB_per_s_algorithmic": round(m["alg_bytes"] / m["elapsed"] / 1e9, 1),
             "stages_ms_per_step_rank0": hl["stages"],
         }

@@ -21,13 +21,24 @@ def _preload_torch_hip_runtime():
         ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
 
 
-# The two library lanes drive four HIP streams beside HIP's own copy traffic;
-# eight hardware queues measured +2-4 % images/s over HIP's default four
-# (DESIGN.md section 12).  HIP reads the variable once, when its runtime
-# initialises, so it is set here, before this package's first HIP call, and
-# only when the process has not chosen a value (a HIP runtime that is
-# already initialised, e.g. by earlier torch.cuda work, keeps its queues).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+def configure_hw_queues(n: int = 8) -> bool:
+    """Opt-in: ask HIP for `n` hardware queues per device (GPU_MAX_HW_QUEUES).
+
+    The two library lanes drive two HIP streams each beside HIP's own copy
+    traffic; eight queues measured +2-4 % images/s over HIP's default four
+    (DESIGN.md section 12), because unrelated streams then stop sharing a
+    queue.  HIP reads the variable once, when its runtime initialises, so this
+    only takes effect if called before the process's first HIP call (this
+    package's or torch's).  Importing the package does NOT set it (it would
+    change every HIP user in the process and leak into child processes);
+    bench.py calls the equivalent itself (--hw-queues).  Returns True when
+    the value was written, False when the process had already chosen one."""
+    if os.environ.get("GPU_MAX_HW_QUEUES"):
+        return False
+    os.environ["GPU_MAX_HW_QUEUES"] = str(int(n))
+    return True
+
+
 _preload_torch_hip_runtime()
 directory = os.path.dirname(os.path.abspath(__file__))
 lib_path = os.path.join(directory, "PhotoHive_DSP_lib/libreport_data.so")

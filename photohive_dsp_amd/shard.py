@@ -50,17 +50,27 @@ def loads(sizes: Sequence[Tuple[int, int]], plan: List[List[int]]) -> List[int]:
 
 
 COUNTERS = ("elapsed", "images", "pixels", "alg_bytes", "kernel_ms", "launches")
+MAX_DEVICES = 64          # device-index slots per node (one-hot, like the wall times)
 
 
-def merge_counters(values, device=None):
+def device_of(local_rank: int, visible: int) -> int:
+    """The device a rank drives: LOCAL_RANK modulo the visible devices (a
+    rehearsal with more ranks than cards puts several ranks on one card; with
+    no device visible, the rank's own index -- the plan of a real node)."""
+    return local_rank % visible if visible > 0 else local_rank
+
+
+def merge_counters(values, device=None, dev_index=None):
     """The single collective: ONE all-reduce (SUM) over the
     default process group (RCCL over xGMI on the GPU box, gloo in the CPU
     tests; identity when torch.distributed is not initialised) of this rank's
     counter vector {elapsed s, images, pixels, algorithmic bytes, kernel ms,
     kernel launches} followed by a one-hot row of world slots holding its wall
-    time at its rank.  Every rank gets the merge: the sums of the counters, the
-    max of the wall times (from the one-hot slots) and each rank's wall time
-    (per_rank_elapsed)."""
+    time at its rank and, when dev_index is given, a one-hot row of device
+    slots.  Every rank gets the merge: the sums of the counters, the max of
+    the wall times (from the one-hot slots), each rank's wall time
+    (per_rank_elapsed), the ranks and the number of DISTINCT devices they ran
+    on (`devices`: a two-rank rehearsal on one card is 2 ranks, 1 device)."""
     import torch
     import torch.distributed as dist
     vals = [float(v) for v in values] + [0.0] * (len(COUNTERS) - len(values))
@@ -68,12 +78,19 @@ def merge_counters(values, device=None):
     world, rank = (dist.get_world_size(), dist.get_rank()) if multi else (1, 0)
     slots = [0.0] * world
     slots[rank] = vals[0]
-    t = torch.tensor(vals + slots, dtype=torch.float64, device=device)
+    devs = [0.0] * MAX_DEVICES
+    if dev_index is not None:
+        if not 0 <= dev_index < MAX_DEVICES:
+            raise ValueError(f"device index {dev_index} outside [0, {MAX_DEVICES})")
+        devs[dev_index] = 1.0
+    t = torch.tensor(vals + slots + devs, dtype=torch.float64, device=device)
     if multi:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     row = t.cpu().tolist()
     res = {k: row[j] for j, k in enumerate(COUNTERS)}
-    per_rank = row[len(COUNTERS):]
+    per_rank = row[len(COUNTERS):len(COUNTERS) + world]
     res["elapsed"] = max(per_rank)
     res["per_rank_elapsed"] = per_rank
+    res["ranks"] = world
+    res["devices"] = sum(1 for x in row[len(COUNTERS) + world:] if x > 0) if dev_index is not None else world
     return res

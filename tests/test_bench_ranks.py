@@ -21,7 +21,7 @@ def test_bench_gpus2_spawns_ranks_and_merges_counters():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout          # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2
+    assert d["n_gpus"] == 2 and d["ranks"] == 2
     assert d["config2"]["images"] == 2 * 8                      # weak: batch 8 per rank
     assert d["config4"]["images"] == 64 and d["config5"]["images"] == 96   # strong: totals split
     from photohive_dsp_amd import shard
@@ -49,3 +49,17 @@ def test_every_roofline_prices_algorithmic_bytes():
     assert bench.algorithmic_bytes("fft_cols", h, w) == 16 * h * (w // 2 + 1)
     assert bench.algorithmic_bytes("blur_path", h, w) == 3 * h * w + 32 * h * (w // 2 + 1)
     assert bench.algorithmic_bytes("report", h, w) == 9 * h * w + 32 * h * (w // 2 + 1)
+
+
+def test_rehearsal_on_one_card_reports_one_gpu():
+    """Two ranks that share one card (a gloo rehearsal on a one-GPU box) are
+    2 ranks on 1 GPU in the line, not "2 GPUs" (VERDICT r5 item 7)."""
+    env = dict(os.environ, PHD_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plan-only",
+                        "--plan-visible-devices", "1", "--batch", "4", "--config4-images", "8",
+                        "--config5-images", "8"], env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert (d["n_gpus"], d["ranks"]) == (1, 2), d
+    assert d["config2"]["images"] == 2 * 4

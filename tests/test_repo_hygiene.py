@@ -51,3 +51,25 @@ def test_production_library_holds_only_launched_kernel_forms():
     assert plans("PHD_CT_COLS") < count.get("k_cols_ct", 0) <= 2 * plans("PHD_CT_COLS"), count
     assert count.get("k_k1t") == 6, count          # <512, tri> and <1024, tri / full>, x SMALL
     assert count.get("k_rgb_stats") == 1, count
+
+
+def test_import_leaves_environment_alone():
+    """Importing the package changes no process-wide setting (VERDICT r5 item
+    7): GPU_MAX_HW_QUEUES stays unset until the caller opts in with
+    configure_hw_queues(), which never overrides a value already chosen."""
+    import subprocess
+    import sys
+    code = ("import os, json; before = dict(os.environ); import photohive_dsp_amd as p; "
+            "after = dict(os.environ); changed = sorted(k for k in set(before) | set(after) "
+            "if before.get(k) != after.get(k)); "
+            "w1 = p.configure_hw_queues(8); v1 = os.environ.get('GPU_MAX_HW_QUEUES'); "
+            "w2 = p.configure_hw_queues(4); v2 = os.environ.get('GPU_MAX_HW_QUEUES'); "
+            "print(json.dumps([changed, w1, v1, w2, v2]))")
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    changed, w1, v1, w2, v2 = json.loads(r.stdout.strip().splitlines()[-1])
+    assert changed == [], changed
+    assert (w1, v1, w2, v2) == (True, "8", False, "8")

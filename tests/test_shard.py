@@ -54,6 +54,12 @@ def _worker(rank, world, port, q):
         el, n, p = m["elapsed"], m["images"], m["pixels"]
         assert m["alg_bytes"] == 3.0 * sum(h * w for h, w in sizes)
         assert m["per_rank_elapsed"] == [0.5 + r for r in range(world)]
+        assert m["ranks"] == world and m["devices"] == world          # no device slots: one per rank
+        # a rehearsal with every rank on one card counts ONE device (bench.py's n_gpus)
+        one = shard.merge_counters([1.0, 1.0], dev_index=shard.device_of(rank, 1))
+        assert (one["ranks"], one["devices"]) == (world, 1), one
+        own = shard.merge_counters([1.0, 1.0], dev_index=shard.device_of(rank, 8))
+        assert (own["ranks"], own["devices"]) == (world, world), own
         got = [None] * world
         dist.all_gather_object(got, mine)
         q.put((rank, el, n, p, got))
