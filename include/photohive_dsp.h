@@ -104,14 +104,18 @@ Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundaries* salien
                                        double magnitude_thresh, int blur_cutoff_ratio_denom);
 
 /* Replaces free_full_report, src/interface.c:97-111: releases the whole tree
- * and sets *report = NULL.  A report of this library is one heap block (every
- * structure and array of the tree inside it), recycled for later reports of
- * the same size; release it only through this call (as the reference's
- * callers do), never by free() on its members (a documented deviation: the
- * reference mallocs each member, src/interface.c:97-111).  A pointer that is
- * not a live report of this library (foreign, or already freed and not yet
- * reused) is ignored; freeing a stale pointer after its block was reused by a
- * later report is undefined, as with free(). */
+ * and sets *report = NULL.
+ *  - A report of get_full_report_data has the reference's allocation shape:
+ *    every structure and array is its own malloc (the blur profile's row
+ *    pointers and each row included), so a C caller may free() a member itself
+ *    (then set it to NULL); this call frees the rest member by member.
+ *  - A report of the batch / u8 entry points (phd_report_*) is one heap block
+ *    holding the whole tree, recycled for later reports of the same size:
+ *    release it only through this call (or phd_free_reports), never by free()
+ *    on a member.
+ * A pointer that is neither (foreign, or already freed) is ignored; freeing a
+ * stale pointer after its memory was reused by a later report is undefined,
+ * as with free(). */
 void free_full_report(Full_Report_Data** report);
 /* free_full_report over an array of n reports (a batch call's `out`); NULL entries are skipped. */
 void phd_free_reports(Full_Report_Data** reports, int n);
@@ -256,6 +260,11 @@ int phd_debug_column_form(int mode);
  * (e^{-i}) in d_out (d_out == d_in allowed).  Returns the plan kind (0 one
  * LDS pass, 1 four-step, 2 Bluestein) or -1. */
 int phd_debug_gfft(const double* d_in, double* d_out, int n, long count);
+
+/* Test hook (no GPU): a report tree in get_full_report_data's allocation shape
+ * (n_palette colours, na x nr bins, n_crops sharpnesses or none when < 0),
+ * filled with a fixed pattern and live for free_full_report. */
+Full_Report_Data* phd_debug_legacy_report(int n_palette, int na, int nr, int n_crops);
 
 /* Free an Image_PGM returned by get_blur_profile_visual. */
 void phd_free_pgm(Image_PGM* img);

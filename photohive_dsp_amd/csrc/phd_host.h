@@ -338,6 +338,13 @@ Full_Report_Data* assemble(const RGB_Statistics& st, double s_bar, const Palette
                            const double* pal, long n_hsv, const BlurTable& tbl, const unsigned long long* bin_sums,
                            double fmax, const phd_config& cfg, const Crop_Boundaries* crops,
                            const double* sharp_sums, std::string* why, double bscale = 0.0);
+// get_full_report_data's reports in the reference's allocation shape
+// (phd_legacy.cpp): a separately malloc'd copy, its registration as a live
+// tree, and its release (false when r is not a live tree)
+Full_Report_Data* legacy_tree_copy(const Full_Report_Data* src);
+void legacy_tree_free(Full_Report_Data* r);
+void legacy_register(const Full_Report_Data* r);
+bool legacy_release(Full_Report_Data* r);
 // get_full_report_data on the caller's planar doubles (phd_planar.cpp): the
 // RGB8 pipeline when every value is k/255.0, else the fp64 planar kernels.
 Full_Report_Data* report_planar(Context* c, const double* r, const double* g, const double* b, int height,

@@ -1076,8 +1076,22 @@ extern "C" Full_Report_Data* get_full_report_data(Image_RGB* image, Crop_Boundar
     // else the reference's fp64 arithmetic on them (phd_planar.cpp)
     Context* c = get_context();
     if (!c) return nullptr;
-    std::lock_guard<std::mutex> lk(c->mu);
-    return report_planar(c, image->r, image->g, image->b, image->height, image->width, cfg, crops);
+    Full_Report_Data* pooled;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        pooled = report_planar(c, image->r, image->g, image->b, image->height, image->width, cfg, crops);
+    }
+    if (!pooled) return nullptr;
+    // the reference's C callers get the reference's allocation shape: every
+    // member its own malloc, so free() of a member is valid (phd_legacy.cpp)
+    Full_Report_Data* tree = legacy_tree_copy(pooled);
+    free_full_report(&pooled);
+    if (!tree) {
+        set_error("report allocation failed");
+        return nullptr;
+    }
+    legacy_register(tree);
+    return tree;
 }
 
 extern "C" void phd_free_reports(Full_Report_Data** reports, int n) {
@@ -1085,10 +1099,16 @@ extern "C" void phd_free_reports(Full_Report_Data** reports, int n) {
 }
 
 extern "C" void free_full_report(Full_Report_Data** report) {
-    // src/interface.c:97-111 frees each structure; every report of this
-    // library is one block (assemble), which goes back to the report pool.
-    // Not a live report of this library (foreign, or already freed): ignored.
+    // src/interface.c:97-111 frees each structure.  A report of the batch
+    // entry points is one block (assemble), which goes back to the report
+    // pool; a report of get_full_report_data is a tree of separate mallocs
+    // (phd_legacy.cpp), freed member by member.  Neither (foreign, or already
+    // freed): ignored, without reading memory around the pointer.
     if (!report || !*report) return;
+    if (legacy_release(*report)) {
+        *report = nullptr;
+        return;
+    }
     char* blk = reinterpret_cast<char*>(*report) - kReportHdr;
     if (!report_pool().give(blk) && getenv("PHD_VERBOSE"))
         fprintf(stderr, "free_full_report: %p is not a live report of this library; ignored\n", (void*)*report);

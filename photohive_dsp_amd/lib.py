@@ -128,6 +128,8 @@ lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
 lib.phd_free_reports.restype = None
 lib.phd_free_reports.argtypes = [P(P(Full_Report_Data)), ctypes.c_int]
 lib.phd_free_pgm.argtypes = [P(Image_PGM)]
+lib.phd_debug_legacy_report.restype = P(Full_Report_Data)
+lib.phd_debug_legacy_report.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
 lib.phd_last_error.restype = ctypes.c_char_p
 lib.phd_device_info.restype = ctypes.c_int
 lib.phd_device_info.argtypes = [ctypes.c_char_p, ctypes.c_int]
