@@ -892,6 +892,9 @@ def main(argv=None):
         else:
             dist.init_process_group(backend)
     cx = Ctx(args, world, rank, backend, dev)
+    if os.environ.get("PHD_BENCH_MAPS"):
+        # the mappings AT a fault (SIGSEGV / SIGABRT ...), written by the library's handler
+        cx.lib.phd_install_crash_maps(f"{os.environ['PHD_BENCH_MAPS']}.fault".encode())
     dump_maps("ctx")
 
     cx.lib.phd_set_lanes(args.lanes)                  # every config of this run
@@ -985,6 +988,9 @@ def main(argv=None):
                     "x_projected_affinity": round(v / cpu["projected_affinity_images_per_s"], 1)}
                 for k, v in ratios.items()}
         print(json.dumps(line), flush=True)
+    # the library's explicit teardown (threads joined, HIP resources released)
+    # before torch's and HIP's own exit handlers; it would also run at exit
+    cx.lib.phd_shutdown()
     if world > 1:
         torch.distributed.destroy_process_group()
     return 0

@@ -304,6 +304,25 @@ int phd_profile_read(int kernel, double* total_ms, long* launches);
  * queries.  Returns the previous setting. */
 int phd_set_lanes(int lanes);
 
+/* Explicit teardown (no counterpart in the reference, which frees per call,
+ * src/interface.c:88-92): joins the library's threads (the second lane's
+ * worker, the host pools) and releases every context's device buffers, pinned
+ * buffers, events and streams after their queued work.  The library registers
+ * it with atexit at its first HIP use, so it also runs before HIP's own
+ * finalizers at exit; a caller may run it earlier (the next call then starts
+ * afresh).  Do not call it while another thread is inside a library call. */
+void phd_shutdown(void);
+
+/* Crash triage: on SIGSEGV / SIGBUS / SIGILL / SIGFPE / SIGABRT write
+ * /proc/self/maps to "<prefix>.<pid>.maps" (async-signal-safe), then hand the
+ * signal to the handler installed before (or the default action).  0 on
+ * success. */
+int phd_install_crash_maps(const char* prefix);
+
+/* Test hook: the library threads alive in this process (lane worker + host
+ * pool threads); start != 0 creates them first. */
+int phd_debug_library_threads(int start);
+
 #ifdef __cplusplus
 }
 #endif

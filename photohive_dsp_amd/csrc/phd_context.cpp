@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstring>
 
+#include <chrono>
+#include <cstdlib>
 #include <thread>
 
 #include <unistd.h>
@@ -16,6 +18,7 @@
 namespace phd {
 
 namespace {
+void register_shutdown();
 thread_local std::string g_error;
 thread_local double g_timings[8];
 thread_local int g_ntimings = 0;
@@ -55,8 +58,14 @@ Context* get_context_lane(int lane) {
     }
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     if (g_ctx[dev][lane]) return g_ctx[dev][lane];
+    // HIP is initialised now (hipGetDevice above): a handler registered here
+    // runs before the finalizers HIP registered at its own start (atexit order
+    // is last-in, first-out), so the library's threads, streams, events and
+    // buffers are released while the runtime is still whole
+    register_shutdown();
     auto* c = new Context();
     c->device = dev;
+    c->pid = getpid();
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         set_error("hipStreamCreate failed");
         delete c;
@@ -112,6 +121,19 @@ std::vector<Context*> device_contexts() {
 
 LaneWorker::LaneWorker() : th_([this] { loop(); }) {}
 
+bool LaneWorker::stop(int timeout_ms) {
+    std::unique_lock<std::mutex> lk(m_);
+    if (!done_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [this] { return !has_job_; })) {
+        th_.detach();
+        return false;
+    }
+    stop_ = true;
+    cv_.notify_all();
+    lk.unlock();
+    th_.join();
+    return true;
+}
+
 void LaneWorker::run(std::function<void()> f) {
     std::lock_guard<std::mutex> lk(m_);
     job_ = std::move(f);
@@ -127,7 +149,8 @@ void LaneWorker::wait() {
 void LaneWorker::loop() {
     std::unique_lock<std::mutex> lk(m_);
     for (;;) {
-        cv_.wait(lk, [this] { return has_job_; });
+        cv_.wait(lk, [this] { return has_job_ || stop_; });
+        if (!has_job_) return;                              // stop()
         std::function<void()> f = std::move(job_);
         lk.unlock();
         f();
@@ -170,18 +193,23 @@ int k1_blocks_per_cu() {
     return env ? env : (t_call_lanes >= 2 ? 1 : 2);
 }
 
+namespace {
+// one lane worker and one decision pool per process (a forked child has none
+// of its parent's threads: it makes its own and never touches the parent's)
+std::mutex g_lw_mu, g_pool_mu;
+LaneWorker* g_lw = nullptr;
+pid_t g_lw_owner = 0;
+HostPool* g_pool = nullptr;
+pid_t g_pool_owner = 0;
+}  // namespace
+
 LaneWorker* lane_worker() {
-    // one per process (a forked child has none of its parent's threads)
-    static std::mutex m;
-    static LaneWorker* w = nullptr;
-    static pid_t owner = 0;
-    std::lock_guard<std::mutex> lk(m);
-    if (!w || owner != getpid()) {
-        w = new LaneWorker();   // never joined: it lives as long as the process
-        w->detach();
-        owner = getpid();
+    std::lock_guard<std::mutex> lk(g_lw_mu);
+    if (!g_lw || g_lw_owner != getpid()) {
+        g_lw = new LaneWorker();   // joined by phd_shutdown (at exit at the latest)
+        g_lw_owner = getpid();
     }
-    return w;
+    return g_lw;
 }
 
 hipStream_t work_stream(Context* c, void* stream) {
@@ -419,7 +447,20 @@ const BlurTable* get_table(Context* c, int height, int width, int nr, int na) {
 }
 
 HostPool::HostPool(int threads) : nthreads_(threads) {
-    for (int t = 0; t < threads; t++) std::thread([this] { worker(); }).detach();
+    for (int t = 0; t < threads; t++) th_.emplace_back([this] { worker(); });
+}
+
+void HostPool::stop() {
+    std::lock_guard<std::mutex> job(job_m_);              // a running job finishes first
+    {
+        std::lock_guard<std::mutex> lk(m_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_)
+        if (t.joinable()) t.join();
+    th_.clear();
+    nthreads_ = 0;
 }
 
 void HostPool::worker() {
@@ -429,7 +470,8 @@ void HostPool::worker() {
         int n;
         {
             std::unique_lock<std::mutex> lk(m_);
-            cv_.wait(lk, [&] { return gen_ != seen; });
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
             seen = gen_;
             fn = fn_;
             n = n_;
@@ -441,7 +483,13 @@ void HostPool::worker() {
 }
 
 void HostPool::parallel_for(int n, const std::function<void(int)>& f) {
-    std::lock_guard<std::mutex> job(job_m_);              // one job at a time (contexts of several devices)
+    // one job at a time; a caller that finds the pool busy (the other lane,
+    // another device's context) runs its items itself rather than wait
+    std::unique_lock<std::mutex> job(job_m_, std::try_to_lock);
+    if (!job.owns_lock() || nthreads_ == 0) {
+        for (int i = 0; i < n; i++) f(i);
+        return;
+    }
     {
         std::lock_guard<std::mutex> lk(m_);
         fn_ = &f;
@@ -458,17 +506,105 @@ void HostPool::parallel_for(int n, const std::function<void(int)>& f) {
 }
 
 HostPool* host_pool() {
-    // one pool per process: a forked child has none of its parent's threads
-    static std::mutex m;
-    static HostPool* p = nullptr;
-    static pid_t owner = 0;
-    std::lock_guard<std::mutex> lk(m);
-    if (!p || owner != getpid()) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_pool || g_pool_owner != getpid()) {
         const unsigned hc = std::thread::hardware_concurrency();
-        p = new HostPool(hc > 1 ? (int)std::min(hc - 1, 7u) : 0);
-        owner = getpid();
+        g_pool = new HostPool(hc > 1 ? (int)std::min(hc - 1, 7u) : 0);
+        g_pool_owner = getpid();
     }
-    return p;
+    return g_pool;
+}
+
+// ---- teardown (phd_shutdown) --------------------------------------------------
+namespace {
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+void ev_destroy(hipEvent_t& e) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+}
+void st_destroy(hipStream_t& s) {
+    if (s) (void)hipStreamDestroy(s);
+    s = nullptr;
+}
+
+// Releases everything a context owns: its queued work is waited for, then its
+// device buffers, pinned buffers, events and streams are released.
+void destroy_context(Context* c) {
+    (void)hipSetDevice(c->device);
+    for (hipStream_t s : {c->stream, c->tail, c->h2d, c->h2d2})
+        if (s) (void)hipStreamSynchronize(s);
+    dfree(c->d_k255);
+    for (auto& kv : c->plans) dfree(kv.second.d_tw);
+    for (auto& kv : c->ct_tw) dfree(kv.second);
+    for (auto& kv : c->tables) dfree(kv.second.d_map);
+    for (auto& kv : c->colruns) {
+        dfree(kv.second.d_runs);
+        dfree(kv.second.d_seg);
+    }
+    for (auto& kv : c->gplans) {
+        dfree(kv.second.d_twn);
+        dfree(kv.second.d_chirp);
+        dfree(kv.second.d_bhat);
+    }
+    for (auto& kv : c->cls) dfree(kv.second.d);
+    dfree(c->d_gbuf);
+    dfree(c->d_planes);
+    dfree(c->d_prec);
+    dfree(c->d_ws);
+    dfree(c->d_inter);
+    dfree(c->d_stage);
+    dfree(c->d_ptrs);
+    for (auto& p : c->d_stage2) dfree(p);
+    if (c->h_pin) (void)hipHostFree(c->h_pin);
+    c->h_pin = nullptr;
+    if (c->h2d_slots) (void)hipHostFree(c->h2d_slots);
+    c->h2d_slots = nullptr;
+    for (auto& e : c->ev) ev_destroy(e);
+    for (hipEvent_t* e : {&c->ev_k1, &c->ev_tail, &c->ev_dl_sd, &c->ev_fft, &c->ev_null, &c->ev_h2d2}) ev_destroy(*e);
+    for (auto& e : c->ev_img_fft) ev_destroy(e);
+    for (auto& e : c->ev_img_dl) ev_destroy(e);
+    for (auto& e : c->ev_slot) ev_destroy(e);
+    for (auto& e : c->ev_up) ev_destroy(e);
+    for (auto& pr : c->prof.pool) {
+        ev_destroy(pr.first);
+        ev_destroy(pr.second);
+    }
+    st_destroy(c->stream);
+    st_destroy(c->tail);
+    st_destroy(c->h2d);
+    st_destroy(c->h2d2);
+}
+
+std::atomic<bool> g_in_exit{false};
+
+void shutdown_at_exit() {
+    g_in_exit.store(true);
+    phd_shutdown();
+}
+
+void register_shutdown() {
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(shutdown_at_exit); });
+}
+
+}  // namespace
+
+int library_threads() {
+    int n = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_lw_mu);
+        n += g_lw && g_lw_owner == getpid();
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_pool && g_pool_owner == getpid()) n += g_pool->size();
+    }
+    return n + copy_pool_threads();
 }
 
 int KernelProfiler::begin(int k, hipStream_t st) {
@@ -531,6 +667,66 @@ const Context::Cls* get_cls(Context* c, const GridParams& gp) {
 }
 
 }  // namespace phd
+
+// The library's explicit teardown (round 6): the lane worker and the host
+// pools' threads are stopped and joined, then every context of this process
+// waits for its streams and releases its device buffers, pinned buffers,
+// events and streams.  Registered with atexit at the first HIP use, so it runs
+// before HIP's own finalizers; callable earlier (then the next call starts
+// afresh).  Not to be called while another thread is inside a library call.
+extern "C" void phd_shutdown(void) {
+    using namespace phd;
+    const pid_t me = getpid();
+    {
+        std::lock_guard<std::mutex> lk(g_lw_mu);
+        if (g_lw && g_lw_owner == me) {
+            if (g_lw->stop(5000)) delete g_lw;   // else left running (a stuck job): not ours to free
+        }
+        g_lw = nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_pool && g_pool_owner == me) {
+            g_pool->stop();
+            delete g_pool;
+        }
+        g_pool = nullptr;
+    }
+    stop_copy_pool();
+    std::vector<Context*> mine;
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        for (auto& per_dev : g_ctx)
+            for (auto& c : per_dev) {
+                if (c && c->pid == me) mine.push_back(c);
+                c = nullptr;                         // another process's (fork): forgotten, never touched
+            }
+    }
+    int dev0 = -1;
+    const bool have_dev = hipGetDevice(&dev0) == hipSuccess;
+    for (Context* c : mine) {
+        // a context still held by a call on another thread is left alone
+        std::unique_lock<std::mutex> lk(c->mu, std::try_to_lock);
+        for (int t = 0; t < 200 && !lk.owns_lock(); t++) {
+            std::this_thread::sleep_for(std::chrono::milliseconds(10));
+            lk.try_lock();
+        }
+        if (!lk.owns_lock()) continue;
+        destroy_context(c);
+        lk.unlock();
+        if (!g_in_exit.load()) delete c;            // at exit its host maps are left to the process
+    }
+    if (have_dev && dev0 >= 0) (void)hipSetDevice(dev0);
+}
+
+extern "C" int phd_debug_library_threads(int start) {
+    if (start) {
+        (void)phd::lane_worker();
+        (void)phd::host_pool();
+        (void)phd::copy_pool();
+    }
+    return phd::library_threads();
+}
 
 extern "C" int phd_set_lanes(int lanes) {
     const int prev = phd::lanes_setting();

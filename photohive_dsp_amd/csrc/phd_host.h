@@ -12,6 +12,8 @@
 #include <tuple>
 #include <vector>
 
+#include <sys/types.h>
+
 #include "../../include/photohive_dsp.h"
 #include "phd_internal.h"
 
@@ -149,8 +151,14 @@ struct KernelProfiler {
 class HostPool {
 public:
     explicit HostPool(int threads);
+    // f(0 .. n-1) on the pool's threads and the caller; a pool busy with
+    // another caller's job (the other lane) runs f inline on the caller instead
+    // of queueing behind it (one lane's assembly no longer waits for
+    // the other lane's palette decisions)
     void parallel_for(int n, const std::function<void(int)>& f);
     int size() const { return nthreads_; }
+    // waits for a running job, then ends and joins the threads (phd_shutdown)
+    void stop();
 
 private:
     void worker();
@@ -161,12 +169,20 @@ private:
     std::atomic<int> next_{0};
     int n_ = 0, busy_ = 0;
     unsigned gen_ = 0;
+    bool stop_ = false;
+    std::vector<std::thread> th_;
 };
 HostPool* host_pool();
 HostPool* copy_pool();   // threads for host-buffer staging copies (phd_upload.cpp)
+// phd_shutdown's parts: join the pools' threads (and forget the pools); the
+// number of live pool threads
+void stop_copy_pool();
+int copy_pool_threads();
+int library_threads();    // lane worker + pool threads alive in this process
 
 struct Context {
     int device = -1;
+    pid_t pid = 0;                                  // the process that created it (phd_shutdown)
     hipStream_t stream = nullptr;
     double* d_k255 = nullptr;                       // k/255.0 for k in [0,256)
     std::map<std::pair<int, bool>, FftPlanHost> plans;   // (length, composite)
@@ -244,7 +260,10 @@ public:
     LaneWorker();
     void run(std::function<void()> f);
     void wait();
-    void detach() { th_.detach(); }
+    // ends the thread after its current job (waiting up to timeout_ms for
+    // it) and joins it; false (thread detached, left to the process) when
+    // the job did not finish in time
+    bool stop(int timeout_ms);
     // one caller at a time owns the worker (run .. wait); a busy worker is
     // not waited for: the caller runs its whole batch on lane 0 instead
     bool try_acquire() { return user_mu_.try_lock(); }
@@ -257,6 +276,7 @@ private:
     std::condition_variable cv_, done_cv_;
     std::function<void()> job_;
     bool has_job_ = false;
+    bool stop_ = false;
     std::thread th_;
 };
 LaneWorker* lane_worker();

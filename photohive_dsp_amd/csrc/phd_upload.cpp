@@ -31,18 +31,35 @@ constexpr size_t kSlotBytes = (size_t)16 << 20;
 constexpr int kSlots = 8;
 }  // namespace
 
+namespace {
+std::mutex g_copy_mu;
+HostPool* g_copy = nullptr;
+pid_t g_copy_owner = 0;
+}  // namespace
+
 HostPool* copy_pool() {
     // the palette decisions own host_pool(); the copies get their own threads
-    static std::mutex m;
-    static HostPool* p = nullptr;
-    static pid_t owner = 0;
-    std::lock_guard<std::mutex> lk(m);
-    if (!p || owner != getpid()) {
+    std::lock_guard<std::mutex> lk(g_copy_mu);
+    if (!g_copy || g_copy_owner != getpid()) {
         const unsigned hc = std::thread::hardware_concurrency();
-        p = new HostPool(hc > 2 ? (int)std::min(hc - 1, 7u) : 0);
-        owner = getpid();
+        g_copy = new HostPool(hc > 2 ? (int)std::min(hc - 1, 7u) : 0);
+        g_copy_owner = getpid();
     }
-    return p;
+    return g_copy;
+}
+
+void stop_copy_pool() {
+    std::lock_guard<std::mutex> lk(g_copy_mu);
+    if (g_copy && g_copy_owner == getpid()) {
+        g_copy->stop();
+        delete g_copy;
+    }
+    g_copy = nullptr;
+}
+
+int copy_pool_threads() {
+    std::lock_guard<std::mutex> lk(g_copy_mu);
+    return g_copy && g_copy_owner == getpid() ? g_copy->size() : 0;
 }
 
 static bool staged_upload() {

@@ -128,6 +128,12 @@ lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
 lib.phd_free_reports.restype = None
 lib.phd_free_reports.argtypes = [P(P(Full_Report_Data)), ctypes.c_int]
 lib.phd_free_pgm.argtypes = [P(Image_PGM)]
+lib.phd_shutdown.restype = None
+lib.phd_shutdown.argtypes = []
+lib.phd_install_crash_maps.restype = ctypes.c_int
+lib.phd_install_crash_maps.argtypes = [ctypes.c_char_p]
+lib.phd_debug_library_threads.restype = ctypes.c_int
+lib.phd_debug_library_threads.argtypes = [ctypes.c_int]
 lib.phd_debug_legacy_report.restype = P(Full_Report_Data)
 lib.phd_debug_legacy_report.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
 lib.phd_last_error.restype = ctypes.c_char_p

@@ -54,3 +54,39 @@ def test_free_full_report_frees_a_legacy_tree_after_member_frees():
     lib.free_full_report(ctypes.byref(rp))
     assert not rp                                   # *report = NULL, as src/interface.c:109
     lib.free_full_report(ctypes.byref(rp))          # NULL: ignored
+
+
+def test_shutdown_joins_library_threads_and_process_exits_cleanly():
+    """phd_shutdown stops and joins the lane worker and
+    both host pools; the library can start them again afterwards, and the
+    process exits 0 with the atexit teardown having nothing left to do.  (No
+    GPU here: the contexts' HIP resources are the -m gpu test's,
+    tests/test_gpu_round6.py.)"""
+    import subprocess
+    import sys
+    code = ("from photohive_dsp_amd.lib import lib; "
+            "a = lib.phd_debug_library_threads(1); lib.phd_shutdown(); b = lib.phd_debug_library_threads(0); "
+            "c = lib.phd_debug_library_threads(1); lib.phd_shutdown(); lib.phd_shutdown(); "
+            "d = lib.phd_debug_library_threads(0); print(a, b, c, d)")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    a, b, c, d = map(int, r.stdout.split())
+    assert a >= 1 and b == 0 and c == a and d == 0, (a, b, c, d)
+
+
+def test_crash_maps_written_at_the_fault(tmp_path):
+    """phd_install_crash_maps: a SIGSEGV writes /proc/self/maps at the fault
+    (async-signal-safe) and the process still dies of the signal."""
+    import signal
+    import subprocess
+    import sys
+    pre = str(tmp_path / "crash")
+    code = ("import ctypes, os; from photohive_dsp_amd.lib import lib; "
+            f"assert lib.phd_install_crash_maps({pre!r}.encode()) == 0; "
+            "ctypes.string_at(0)")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == -signal.SIGSEGV, (r.returncode, r.stderr[-2000:])
+    maps = [p for p in os.listdir(tmp_path) if p.endswith(".maps")]
+    assert len(maps) == 1, maps
+    txt = (tmp_path / maps[0]).read_text()
+    assert "libreport_data.so" in txt and "[stack]" in txt
