@@ -60,6 +60,18 @@ __device__ __forceinline__ int code_idx(int kmx, int kd) {
     else return (kmx << 8) | kd;
 }
 
+// code_idx for the two pixels of a u16 pair at once (u16 lanes: no overflow,
+// kmx (kmx + 1) <= 65280)
+template <bool TRI>
+__device__ __forceinline__ u16x2 code_idx2(u16x2 mx, u16x2 kd) {
+    const u16x2 one = {1, 1};
+    if constexpr (TRI) return ((mx * (mx + one)) >> one) + kd;
+    else {
+        const u16x2 eight = {8, 8};
+        return (mx << eight) | kd;
+    }
+}
+
 constexpr int kCellBytes = 24;   // {u64 count word, f64 sum h, f64 sum s}
 
 // LDS carve (bytes).
@@ -121,7 +133,7 @@ template <bool TRI, bool SMALL, bool MERGE>
 __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
                                              const unsigned char* __restrict__ code8,
                                              unsigned char* __restrict__ cells, int cshift, int copy,
-                                             const K1Grid& G, CellRun* run = nullptr, unsigned* same = nullptr) {
+                                             const K1Grid& G, CellRun* run, unsigned& nsame) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
     const u16x2 r13 = as2(__builtin_amdgcn_perm(w2, w0, 0x0c050c03u));
@@ -149,31 +161,42 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
     const unsigned Kd[2] = {as1(mx02 - mn02), as1(mx13 - mn13)};
     const unsigned R[2] = {as1(r02), as1(r13)}, Gc[2] = {as1(g02), as1(g13)}, B[2] = {as1(b02), as1(b13)};
     // the four code reads first: LDS operations complete in order, so a read
-    // placed after an atomic would wait for it
+    // placed after an atomic would wait for it.  The table index of both
+    // pixels of a pair in packed u16 arithmetic (round 6: kmx (kmx + 1) / 2 +
+    // kd <= 32895, three v_pk ops per pair instead of five VALU per pixel)
+    const u16x2 kd02 = mx02 - mn02, kd13 = mx13 - mn13;
+    const unsigned Ix[2] = {as1(code_idx2<TRI>(mx02, kd02)), as1(code_idx2<TRI>(mx13, kd13))};
     int code[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);           // pixel i: pair q, half i >> 1
-        code[i] = code8[code_idx<TRI>((Mx[q] >> sh) & 0xFFFF, (Kd[q] >> sh) & 0xFFFF)];
+        code[i] = code8[(Ix[q] >> sh) & 0xFFFF];
     }
     K1Inv ekd[4];
-    double ikm[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
         // from the VALU (round 4: an LDS table of reciprocals measured slower,
-        // 46 against 40 us per image -- the LDS is the busier pipe)
-        ekd[i] = k1_inv_valu(kd > 1 ? kd : 1);
-        ikm[i] = k1_inv_valu(kmx > 1 ? kmx : 1).inv;
+        // 46 against 40 us per image -- the LDS is the busier pipe); one
+        // reciprocal of kd kmax per pixel since round 6
+        ekd[i] = k1_inv_pair(kd > 1 ? kd : 1, kmx > 1 ? kmx : 1);
     }
+    // X of both pixels of each pair in 16-bit lanes (k1_x_pair)
+    const unsigned Xp[2] = {as1(k1_x_pair(r02, g02, b02, mx02, kd02)), as1(k1_x_pair(r13, g13, b13, mx13, kd13))};
     unsigned def = 0;
+    int cell0 = 0;
+    bool same = true;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);
-        const int kr = (R[q] >> sh) & 0xFFFF, kg = (Gc[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
         const int kmx = (Mx[q] >> sh) & 0xFFFF, kmn = (Mn[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
-        const K1Px p = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kd, code[i], ekd[i], ikm[i], G);
+        bool special = false;
+        if constexpr (!SMALL) {
+            const int kr = (R[q] >> sh) & 0xFFFF, kg = (Gc[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
+            special = (kr == kg) | (kg == kb) | (kr == kb);
+        }
+        const K1Px p = k1_pixel_x<SMALL>((int)((Xp[q] >> sh) & 0xFFFF), special, kmx, kmn, kd, code[i], ekd[i], G);
         if constexpr (MERGE) {
             if (p.cell == run->cell) {
                 run->lo += p.lo;
@@ -191,18 +214,20 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
         } else {
             cell_add(cells, p.cell, cshift, copy, p);
         }
-        def |= (unsigned)(p.cell == G.ncell) << i;
-        if (same) {                                       // all four pixels in one cell (the MG 2 sample)
-            if (i == 0) *same = (unsigned)p.cell;
-            else if (*same != (unsigned)p.cell) *same = ~0u;
-        }
+        def |= p.dfr << i;
+        // the vote sample: are all four pixels in one cell?  (every group
+        // since round 6: a sample of step 0 only cost two selects per pixel in
+        // every step of the un-unrolled loop)
+        if (i == 0) cell0 = p.cell;
+        else same = same && p.cell == cell0;
     }
-    if (same) *same = *same != ~0u;
+    nsame += same ? 1u : 0u;
     return def;
 }
 
 // Per-thread cell runs (CellRun) for the next chunk when more than a fifth of
-// this chunk's sampled 4-pixel groups (each thread's first) lie in one cell,
+// this chunk's 4-pixel groups lie in one cell (round 6: every group counted;
+// before, each thread's first only),
 // else every pixel's atomics -- flat images (SURVEY 8(d) row 2(b)'s blurred
 // structured ones: 81 % of groups) pay for the runs' selects, noise does not
 // (round 4: runs always 43.8 against 40.6 us on noise, never 80 against 48
@@ -301,7 +326,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             unsigned a0 = p_ok ? p0 : 0u, a1 = p_ok ? p1 : 0u, a2 = p_ok ? p2 : 0u;
             if (!have_pf) ld(0, a0, a1, a2);
             CellRun run{-1, 0u, 0u, 0.0, 0.0};
-            unsigned same0 = 0;
+            unsigned nsame = 0;                                   // this thread's groups in one cell
             auto loop = [&](auto mg) __attribute__((always_inline)) {
                 constexpr bool M = decltype(mg)::value;
 #pragma unroll 1
@@ -309,8 +334,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                     // the next group (the last step reloads its own: unused)
                     unsigned n0, n1, n2;
                     const bool nok = ld_raw(st + 1 < kG ? st + 1 : st, n0, n1, n2);
-                    emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, cells, cshift, copy, G, &run,
-                                                     st == 0 ? &same0 : nullptr)
+                    emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, cells, cshift, copy, G, &run, nsame)
                              << (4 * st);
                     a0 = nok ? n0 : 0u;
                     a1 = nok ? n1 : 0u;
@@ -324,8 +348,8 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             };
             if (merge) loop(std::true_type{});
             else loop(std::false_type{});
-            const unsigned long long b = __ballot(same0);
-            if (lane_id() == 0) atomicAdd(&vote[16 * vpar], (unsigned)__popcll(b));
+            const unsigned long long nw = wave_sum((unsigned long long)nsame);
+            if (lane_id() == 0) atomicAdd(&vote[16 * vpar], (unsigned)nw);
         }
         const bool last_chunk = base + kChunk >= npix;            // block-uniform
         if (last_chunk && tid == 0) {
@@ -338,8 +362,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                 const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
                 const int code = code8[code_idx<TRI>(kmx, kmx - kmn)];
                 K1Px px = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kmx - kmn, code,
-                                          k1_inv_valu(kmx - kmn > 1 ? kmx - kmn : 1),
-                                          k1_inv_valu(kmx > 1 ? kmx : 1).inv, G);
+                                          k1_inv_pair(kmx - kmn > 1 ? kmx - kmn : 1, kmx > 1 ? kmx : 1), G);
                 if (px.cell == ncell) px = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
                 cell_add(cells, px.cell, cshift, copy, px);
             }
@@ -401,7 +424,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             p2 = q[2];
         }
         __syncthreads();
-        merge = 5 * vote[16 * vpar] > (unsigned)kT;              // the next chunk's mode
+        merge = 5 * vote[16 * vpar] > (unsigned)(kT * kG);       // the next chunk's mode: > 1/5 of groups
         // fold the chunk's count words: one thread per cell sums its C copies;
         // the run's cell counts, the chunk's group counts, per-group sum kmax / n255
         for (int q = tid; q <= ncell; q += kT) {
@@ -618,10 +641,20 @@ int k1_host_pixels(const GridParams& gp, const ClassTables& t, const uint8_t* rg
         const int kr = rgb[3 * i], kg = rgb[3 * i + 1], kb = rgb[3 * i + 2];
         const int kmx = std::max(kr, std::max(kg, kb)), kmn = std::min(kr, std::min(kg, kb)), kd = kmx - kmn;
         const int code = t.code8[kmx * 256 + kd];
-        const K1Inv ekd = k1_inv_valu(kd > 1 ? kd : 1);          // as the production kernel (RT false)
-        const double ikm = k1_inv_valu(kmx > 1 ? kmx : 1).inv;
-        K1Px p = G.small_c ? k1_pixel<true>(kr, kg, kb, kmx, kmn, kd, code, ekd, ikm, G)
-                           : k1_pixel<false>(kr, kg, kb, kmx, kmn, kd, code, ekd, ikm, G);
+        const K1Inv e = k1_inv_pair(kd > 1 ? kd : 1, kmx > 1 ? kmx : 1);   // as the production kernel
+        // X through the kernel's packed pair form (this pixel in the high
+        // half, its channel-rotated twin in the low half: both lanes checked)
+        const k1_u16x2 r2 = {(unsigned short)kg, (unsigned short)kr}, g2 = {(unsigned short)kb, (unsigned short)kg},
+                       b2 = {(unsigned short)kr, (unsigned short)kb};
+        const k1_u16x2 m2 = {(unsigned short)kmx, (unsigned short)kmx}, d2 = {(unsigned short)kd, (unsigned short)kd};
+        const k1_u16x2 x2 = k1_x_pair(r2, g2, b2, m2, d2);
+        const int X = x2[1];
+        const bool special = (kr == kg) | (kg == kb) | (kr == kb);
+        if (x2[0] != k1_x_pair((k1_u16x2){(unsigned short)kg, 0}, (k1_u16x2){(unsigned short)kb, 0},
+                               (k1_u16x2){(unsigned short)kr, 0}, m2, d2)[0])
+            return -2;                                   // the two lanes of a pair disagree
+        K1Px p = G.small_c ? k1_pixel_x<true>(X, special, kmx, kmn, kd, code, e, G)
+                           : k1_pixel_x<false>(X, special, kmx, kmn, kd, code, e, G);
         const bool def = p.cell == G.ncell;
         if (def) p = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
         cell[i] = p.cell;

@@ -40,6 +40,7 @@ namespace phd {
 struct K1Grid {
     int lh;          // Lh = 360 / h_partitions (integer, color_quantization.c:41)
     float rlh;       // 1 / Lh in fp32 (k1_halfbin)
+    float rlh2;      // rlh / 2 (exact): the fast path's half-bin quotient (k1_pixel)
     int hp, hp2;     // h_partitions, 2 h_partitions
     int spvp;        // colour codes: 0 .. spvp - 1
     int ac;          // 4 spvp - 2: cell step per hue bin of a colour code
@@ -61,30 +62,48 @@ K1_HD int k1_mul(int a, int b) {
 #endif
 }
 
-// The reciprocals a pixel needs, per k in [1, 255]: 1 / k to double (h = 60 X
-// / kd and s = kd / kmax as one multiply each, within an ulp of the exact
-// rational) and to float (the half-bin cell's fp32 quotient).
+// The one reciprocal a pixel needs (round 6; two before): r = 1 / (kd1 km1)
+// with kd1 = max(kd, 1), km1 = max(kmax, 1) (kd1 km1 <= 65025, exact in fp32),
+// from the fp32 reciprocal and one fp64 Newton step (1 - p r is exact in an
+// fma; ~2^-45 relative).  h = 60 X / kd = (60 X km1) r and s = kd / kmax =
+// kd^2 r then take one fp64 multiply of an exact integer each, and the fp32
+// 1 / kd of the half-bin quotient is km1 * (fp32 r).  (Two reciprocals cost
+// eight fp64 instructions per pixel, this one four; fp64 issues at half rate.)
 struct K1Inv {
-    double inv;
-    float rcp;
+    double inv;      // 1 / (kd1 km1)
+    float rkd;       // 1 / kd1 in fp32: <= 1.5 ulp on the device, 1 ulp on the host
     unsigned pad;
 };
-// From the VALU: the fp32 reciprocal and one fp64 Newton step (1 - k r is
-// exact in an fma; ~2^-45 relative), no table read.
-K1_HD K1Inv k1_inv_valu(int k) {
+K1_HD K1Inv k1_inv_pair(int kd1, int km1) {
+    const int p = k1_mul(kd1, km1);
+    const float pf = (float)p;
 #if defined(__HIP_DEVICE_COMPILE__)
-    const float r = __builtin_amdgcn_rcpf((float)k);
+    const float r = __builtin_amdgcn_rcpf(pf);
 #else
-    const float r = 1.0f / (float)k;
+    const float r = 1.0f / pf;
 #endif
+    // the Newton residual 1 - p r in ONE fp32 fma (p r exact inside it; |1 - p
+    // r| <= 2^-23, so its fp32 rounding errs by <= 2^-47), then r (1 + e) in
+    // fp64: three fp64 instructions instead of four, ~2^-46 relative
+    const float e = std::fma(-pf, r, 1.0f);
     const double d = (double)r;
-    const double e = std::fma(-(double)k, d, 1.0);
-    return K1Inv{std::fma(d, e, d), r, 0u};
+    return K1Inv{std::fma(d, (double)e, d), (float)km1 * r, 0u};
+}
+
+// q - floor(q) for 0 <= q < 2^23 (exact in fp32)
+K1_HD float k1_fract(float q, int c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    (void)c;
+    return __builtin_amdgcn_fractf(q);
+#else
+    return q - (float)c;
+#endif
 }
 
 K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
     G.lh = 360 / g.hp;
     G.rlh = 1.0f / (float)G.lh;
+    G.rlh2 = 0.5f * G.rlh;
     G.hp = g.hp;
     G.hp2 = 2 * g.hp;
     G.spvp = g.sp * g.vp;
@@ -119,38 +138,86 @@ K1_HD int k1_halfbin(int n2, float rkd, const K1Grid& G) {
 
 struct K1Px {
     int cell;        // ncell when deferred
+    unsigned dfr;    // 1 when deferred
     unsigned lo, hi; // the cell word: lo = 1 | (kmax == 255) << 16, hi = kmax
     double h, s;
 };
 
-// The fast path.  kd = kmx - kmn; code = the table's byte for (kmx, kd); ekd
-// = the K1Inv entry of max(kd, 1), ikm = 1 / max(kmx, 1) (the caller reads
-// them with the code, ahead of the previous pixels' LDS atomics).  Deferred
-// pixels get cell = ncell (their count and sums land in the dummy cell, never
-// read) and are redone by k1_exact.
+typedef unsigned short k1_u16x2 __attribute__((ext_vector_type(2)));
+typedef short k1_i16x2 __attribute__((ext_vector_type(2)));
+
+// X = sector kd + num (k1_pixel) for the two pixels of a u16 pair at once, in
+// 16-bit lanes (round 6; v_pk_* ops on the device, ~8 VALU per pixel instead
+// of ~15): the three branch values, and the first-max selection by masks --
+// (max - 1) - channel is -1 exactly where that channel is the max (it is
+// never below -1), so its arithmetic shift by 15 is the all-ones select mask.
+// All values fit i16 (|X| < 6 * 256).
+// The all-ones mask of each 16-bit lane of x that is negative.  On the device
+// an opaque v_pk_ashrrev_i16: the compiler would otherwise see the sign splat,
+// turn the mask-and-merge below into per-lane compares and selects and repack
+// the halves (13 VALU per pair instead of 4).
+K1_HD k1_i16x2 k1_neg_mask(k1_i16x2 x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned r;
+    asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(__builtin_bit_cast(unsigned, x)));
+    return __builtin_bit_cast(k1_i16x2, r);
+#else
+    return x >> (k1_i16x2){15, 15};
+#endif
+}
+
+K1_HD k1_u16x2 k1_x_pair(k1_u16x2 r, k1_u16x2 g, k1_u16x2 b, k1_u16x2 mx, k1_u16x2 kd) {
+    const k1_i16x2 R = __builtin_bit_cast(k1_i16x2, r), Gc = __builtin_bit_cast(k1_i16x2, g),
+                   B = __builtin_bit_cast(k1_i16x2, b), K = __builtin_bit_cast(k1_i16x2, kd);
+    const k1_i16x2 m1 = __builtin_bit_cast(k1_i16x2, mx) - (k1_i16x2){1, 1};
+    const k1_i16x2 sh15 = {15, 15};
+    const k1_i16x2 mr = k1_neg_mask(m1 - R);                   // -1: r is the max (first)
+    const k1_i16x2 mg = k1_neg_mask(m1 - Gc);                  // -1: g is the max
+    const k1_i16x2 d = Gc - B;
+    const k1_i16x2 xr = d + ((d >> sh15) & (K * (k1_i16x2){6, 6}));   // g - b, + 6 kd when negative
+    const k1_i16x2 xg = (K << (k1_i16x2){1, 1}) + B - R;
+    const k1_i16x2 xb = (K << (k1_i16x2){2, 2}) + R - Gc;
+    const k1_i16x2 X = (mr & xr) | (~mr & ((mg & xg) | (~mg & xb)));
+    return __builtin_bit_cast(k1_u16x2, X);
+}
+
+// The fast path.  kd = kmx - kmn; code = the table's byte for (kmx, kd); e =
+// k1_inv_pair(max(kd, 1), max(kmx, 1)) (the caller computes it with the code
+// read, ahead of the previous pixels' LDS atomics).  Deferred pixels get cell
+// = ncell (their count and sums land in the dummy cell, never read) and are
+// redone by k1_exact.
+//
+// The half-bin cell and the boundary test (round 6): with u = 1 / (Lh kd1),
+// the exact quotient q* = (n2 + 1/2) u = m + (j + 1/2) u, m = floor(n2 u), j =
+// n2 mod (Lh kd1); the pixel is on a boundary (onb) iff j = 0.  The fp32 q =
+// (2 n2 + 1) * (rlh/2 * rkd) errs by at most ~3 ulp = 3.6e-7 q* relative (2 n2
+// + 1 exact, rlh/2 0.5 ulp, rkd 1.5, two products 0.5 each); as q* < 720 / Lh
+// + 1 and u >= 1 / (255 Lh), that is at most 3.6e-7 (720 + Lh) 255 u <= 0.1 u
+// for every Lh <= 360 and kd <= 255.  So c = (int)q = m, and fract(q) lies within 0.1 u of (j + 1/2) u: in
+// [0.4 u, 0.6 u] on a boundary, >= 1.4 u off it; the threshold thr = 2 (rlh/2
+// rkd) = u (1 +- 3e-7) splits them with 0.4 u to spare on both sides, on the
+// device (v_rcp_f32, 1 ulp) and on the host (correctly rounded) alike.  (Before
+// round 6: onb = (c Lh kd1 == n2), one quarter-rate v_mul_lo_u32 per pixel.)
+//
+// k1_pixel_x takes X from k1_x_pair (the kernel) and `special` (two channels
+// equal; read only by the !SMALL form); k1_pixel computes both itself.
 template <bool SMALL>   // SMALL == G.small_c
-K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, const K1Inv& ekd, double ikm,
-                    const K1Grid& G) {
-    const int kd1 = kd > 1 ? kd : 1;
-    const bool isr = kr == kmx, isg = kg == kmx;
-    // X = sector kd + num: rgb2hsv's three branches (max == r first, then g)
-    const int t1 = isg ? kb - kr : kr - kg;
-    const int xs = (kd << (isg ? 1 : 2)) + t1;
-    const int xr = kg - kb + (kg < kb ? k1_mul(6, kd) : 0);
-    const int X = isr ? xr : xs;
-    const int n2 = k1_mul(120, X);
-    const int D = k1_mul(G.lh, kd1);
-    const int c = k1_halfbin(n2, ekd.rcp, G);
-    const bool onb = k1_mul(c, D) == n2;
-    bool below, def;
+K1_HD K1Px k1_pixel_x(int X, bool special, int kmx, int kmn, int kd, int code, const K1Inv& e,
+                      const K1Grid& G) {
+    const int km1 = kmx > 1 ? kmx : 1;
+    const float thr2 = G.rlh2 * e.rkd;                          // u / 2
+    // (2 n2 + 1) u / 2 with one rounding: the fma of the exact 240 X
+    const float q = std::fma((float)k1_mul(240, X), thr2, thr2);   // (n2 + 1/2) u, n2 = 120 X
+    const int c = (int)q;
+    const unsigned onb = k1_fract(q, c) < thr2 + thr2 ? 1u : 0u;
+    unsigned below, def;        // 0 / 1
     if (SMALL) {
         // one 64-bit shift of a uniform mask per property (v_lshrrev_b64; the
         // two 32-bit words selected by c >= 32 cost a compare, two moves of
-        // the words and a select each)
-        below = onb && (unsigned)(G.below_m >> c) & 1u;
-        def = onb && (unsigned)(G.defer_m >> c) & 1u;
+        // the words and a select each), its low bit masked by onb
+        below = onb & (unsigned)(G.below_m >> c);
+        def = onb & (unsigned)(G.defer_m >> c);
     } else {
-        const bool special = (kr == kg) | (kg == kb) | (kr == kb);
         const int ch = c - G.hp;
         below = onb && special && ch >= 0 && ((ch & 1) || ch == 0);
         def = onb && !special;
@@ -159,16 +226,30 @@ K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, 
     // colour: 4 (hi spvp + code) + 1 + (c - 2 hi); gray / black: 4 gs + j 2 hp + c
     const int mul = color ? 4 : G.hp2;
     const int add = color ? k1_mul(c >> 1, G.ac) + 1 : G.gray_cb;
-    const int cell = k1_mul(code, mul) + add + c - (below ? 1 : 0);
+    const int cell = k1_mul(code, mul) + add + c - (int)below;
     K1Px p;
     p.cell = def ? G.ncell : cell;
+    p.dfr = def;
     p.lo = 1u + ((unsigned)((kmx + 1) >> 8) << 16);
     p.hi = (unsigned)kmx;
     // rgb2hsv: h = 60 X / kd (0 for kd = 0); s = kd / kmx, 0.999999 when
     // min == 0 < max (src/image_processing.c:408-414), 0 for black
-    p.h = (double)k1_mul(60, X) * ekd.inv;
-    p.s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)kd * ikm;     // black: kd = 0
+    p.h = (double)k1_mul(k1_mul(X, km1), 60) * e.inv;       // 60 X km1 < 2^25
+    p.s = (kmn == 0 && kmx != 0) ? 0.999999 : (double)k1_mul(kd, kd) * e.inv;     // black: kd = 0
     return p;
+}
+
+template <bool SMALL>
+K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, const K1Inv& e,
+                    const K1Grid& G) {
+    const bool isr = kr == kmx, isg = kg == kmx;
+    // X = sector kd + num: rgb2hsv's three branches (max == r first, then g)
+    const int t1 = isg ? kb - kr : kr - kg;
+    const int xs = (kd << (isg ? 1 : 2)) + t1;
+    const int xr = kg - kb + (kg < kb ? k1_mul(6, kd) : 0);
+    const int X = isr ? xr : xs;
+    const bool special = (kr == kg) | (kg == kb) | (kr == kb);
+    return k1_pixel_x<SMALL>(X, special, kmx, kmn, kd, code, e, G);
 }
 
 // A deferred pixel: rgb2hsv's double hue (the reference's expression on the
@@ -215,6 +296,7 @@ K1_HD K1Px k1_exact(int kr, int kg, int kb, int code, double Lh, const double* k
     } else {
         p.cell = G.gray_cb + code * G.hp2 + cg;
     }
+    p.dfr = 0u;
     p.lo = 1u + ((unsigned)((kmx + 1) >> 8) << 16);
     p.hi = (unsigned)kmx;
     p.h = h;
