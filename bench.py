@@ -278,8 +278,13 @@ def algorithmic_bytes(kernel, h, w):
     column pass (its polar-bin runs, ~1.5 MB per size shared by every image, are
     an implementation table, not counted)."""
     n, hwf = h * w, h * (w // 2 + 1)
+    # report_design: the bytes this build's report moves -- SURVEY 8(d)'s 9 N
+    # counts a second RGB8 read for the palette's calculate_avg_hsv pass, which
+    # the one-pass palette (K1 sums h / s / v per hue cell) does not make; the
+    # tie-overflow walk (k_partial_sums_img) reads only a prefix of some images
     return {"hsv_stats": 3 * n, "palette_sums": 3 * n, "fft_rows": 3 * n + 16 * hwf,
-            "fft_cols": 16 * hwf, "blur_path": 3 * n + 32 * hwf, "report": 9 * n + 32 * hwf}[kernel]
+            "fft_cols": 16 * hwf, "blur_path": 3 * n + 32 * hwf, "report": 9 * n + 32 * hwf,
+            "report_design": 6 * n + 32 * hwf}[kernel]
 
 
 def per_kernel_roofline(warm, B, H, W):
@@ -299,10 +304,17 @@ def per_kernel_roofline(warm, B, H, W):
 
 
 def pipeline_roofline(images_per_s, H, W):
-    """The whole report against HBM: images/s x SURVEY.md 8(d)'s 9 N + 32 H Wf bytes."""
+    """The whole report against HBM: images/s x SURVEY.md 8(d)'s 9 N + 32 H Wf
+    bytes (`frac`), and beside it on the bytes this design moves, 6 N + 32 H Wf
+    (`frac_design_bytes`: no second RGB8 pass for the palette sums)."""
     gbs = images_per_s * algorithmic_bytes("report", H, W) / 1e9
+    gbs_d = images_per_s * algorithmic_bytes("report_design", H, W) / 1e9
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_image": algorithmic_bytes("report", H, W)}
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_image": algorithmic_bytes("report", H, W),
+            "achieved_design_bytes": round(gbs_d, 1), "frac_design_bytes": round(gbs_d / HBM_PEAK_GBS, 4),
+            "design_bytes_per_image": algorithmic_bytes("report_design", H, W),
+            "design_bytes_note": "SURVEY 8(d)'s 9N + 32HWf less the 3N palette pass-2 re-read this build does not "
+                                 "make (K1 sums h/s/v per hue cell in its one pass)"}
 
 
 def pmc_traffic(args, H, W):

@@ -7,7 +7,7 @@ FETCH_SIZE reads half the bytes of wide coalesced streaming reads on gfx950,
 so the read side is doubled.  Writes profiles/pmc_latest.json (+ a copy named
 by --tag) for bench.py's roofline.traffic.
 
-    python tools/pmc_collect.py --tag r01 -- --steps 2 --warmup 1 --batch 4
+    python tools/pmc_collect.py --tag r06 -- --steps 1 --warmup 1 --batch 512 --lanes 2 --no-configs --no-one-lane
 """
 import argparse
 import csv
@@ -20,7 +20,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"k_k1t": "hsv_stats", "k_rgb_stats": "rgb_stats", "k_hsv_stats": "hsv_stats", "k_fft_rows": "fft_rows", "k_fft_cols": "fft_cols",
          "k_rows_ct": "fft_rows", "k_cols_ct": "fft_cols", "k_cutoffs_b": "palette_cutoffs",
-         "k_palette_sums_b": "palette_sums",
+         "k_palette_sums_b": "palette_sums", "k_partial_sums_img": "palette_partial_sums",
+         "k_partial_sums_b": "palette_partial_sums",
          "k_cutoffs": "palette_cutoffs", "k_palette_sums": "palette_sums", "k_sharp_pass": "sharpness"}
 
 
@@ -33,7 +34,7 @@ def short(name):
 
 def run_pass(counter, outdir, bench_args):
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
-           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-kernel-events", "--lanes", "1"] + bench_args
+           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-kernel-events"] + bench_args
     subprocess.run(cmd, check=True, cwd=ROOT)
     files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -62,9 +63,14 @@ def main():
     sys.path.insert(0, ROOT)
     from bench import parse as bench_parse
     ba = bench_parse(bench_args)
-    images = ba.batch * (ba.steps + max(1, ba.warmup))     # every step, warmup included, is profiled
+    # images profiled: one row-pass launch per image at the compile-time sizes
+    # (every step of the run, warm-up and timing steps alike); the arithmetic
+    # count as a fallback
+    images = fetch["fft_rows"][1] if "fft_rows" in fetch else ba.batch * (ba.steps + max(1, ba.warmup))
     res = {"image": f"{a.height}x{a.width}", "source": [os.path.relpath(f1, ROOT), os.path.relpath(f2, ROOT)],
-           "bench_args": bench_args,
+           "bench_args": bench_args, "images_profiled": images,
+           "note": "rocprofv3 --pmc serialises kernel dispatches, so the two lanes' kernels (bench --lanes) ran one "
+                   "at a time in these passes; each kernel's bytes per image are its own",
            "correction": "hbm_bytes = fetch_factor*FETCH_SIZE*1024 + WRITE_SIZE*1024 (fetch_factor 2 for streaming "
                          "reads, MI355X_MICROARCH.md; calibrated per FFT pass where profiles/pmc_calib.json has it)",
            "kernels": {}}
@@ -84,7 +90,7 @@ def main():
         pass
     for k in sorted(set(fetch) | set(write)):
         (fk, n), (wk, _) = fetch.get(k, (0.0, 0)), write.get(k, (0.0, 0))
-        per_launch = images / max(n, 1)
+        per_launch = images / max(n, 1)              # images per launch (< 1: several launches per image)
         fac = factors.get(k, 2.0)
         hbm = fac * fk * 1024 + wk * 1024
         res["kernels"][k] = {"fetch_size_kb": fk, "write_size_kb": wk, "launches": n, "fetch_factor": fac,
