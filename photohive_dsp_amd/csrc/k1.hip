@@ -72,18 +72,32 @@ __device__ __forceinline__ u16x2 code_idx2(u16x2 mx, u16x2 kd) {
     }
 }
 
-constexpr int kCellBytes = 24;   // {u64 count word, f64 sum h, f64 sum s}
-
 // LDS carve (bytes).
-constexpr int kDq = 128;         // deferred-pixel queue entries per wave (u16 chunk offsets)
+constexpr int kDq = 48;          // deferred-pixel queue entries per wave (u16 chunk offsets; ~35 per chunk)
+
+// The accumulators (round 6; before, one 24-byte {count, sum h, sum s} record
+// per hue cell and lane copy, whose random addresses cost LDS bank conflicts):
+//  * per hue cell and lane copy (cs: log2 copies) the u64 count word,
+//    cnt[(cell << cs) | copy];
+//  * per GROUP and lane copy (hs: log2 copies, up to 16) fp64 sum h and sum s,
+//    hsum[(g << hs) | copyh], the s array soff bytes after it.  Only counts
+//    are needed per cell (calculate_avg_hsv's wrap sides, fused_slot_sums);
+//    h and s per group.  With 16 copies indexed by lane & 15 every lane of an
+//    instruction's 16-lane group hits its own bank pair: conflict-free.
+// The launch picks (cs, hs) by an expected-conflict cost (k1_config).
+__host__ __device__ inline int k1_cfg(int cs, int hs) { return cs | (hs << 4); }
+__host__ __device__ inline int k1_cs(int cfg) { return cfg & 15; }
+__host__ __device__ inline int k1_hs(int cfg) { return cfg >> 4; }
 
 struct LVar {
-    int cells, code, k255, red, dq, rcell, cg, seg, r255, rmx, gacc, end;
+    int cells, hsum, soff, code, k255, red, dq, rcell, cg, seg, r255, rmx, end;
 };
-__host__ __device__ inline LVar l_var(int tl, int ncell, int cshift, int code_bytes) {
+__host__ __device__ inline LVar l_var(int tl, int ncell, int cfg, int code_bytes) {
     LVar v;
-    v.cells = 0;                                                    // (ncell + 1) << cshift cells
-    v.code = (kCellBytes * ((ncell + 1) << cshift) + 15) & ~15;     // code_bytes u8
+    v.cells = 0;                                                    // (ncell + 1) << cs u64 count words
+    v.hsum = (8 * ((ncell + 1) << k1_cs(cfg)) + 15) & ~15;          // (tl + 1) << hs f64 sum h, then sum s
+    v.soff = 8 * ((tl + 1) << k1_hs(cfg));
+    v.code = v.hsum + 2 * v.soff;                                   // code_bytes u8
     v.k255 = (v.code + code_bytes + 15) & ~15;                      // 256 f64: k / 255.0 (deferred pixels)
     v.red = v.k255 + 2048;                                          // 16 waves x 8 u64
     v.dq = v.red + 1024;                                            // 16 waves x kDq u16: deferred pixels
@@ -92,8 +106,7 @@ __host__ __device__ inline LVar l_var(int tl, int ncell, int cshift, int code_by
     v.seg = v.cg + 4 * tl;                                          // tl u32: the run's group counts
     v.r255 = v.seg + 4 * tl;                                        // tl u32: the run's #(kmax == 255)
     v.rmx = (v.r255 + 4 * tl + 7) & ~7;                             // tl u64: the run's sum kmax
-    v.gacc = v.rmx + 8 * tl;                                        // 2 tl f64: the run's sum h, sum s
-    v.end = v.gacc + 16 * tl;
+    v.end = v.rmx + 8 * tl;
     return v;
 }
 
@@ -104,14 +117,24 @@ __device__ __forceinline__ int group_of_cell(int q, const K1Grid& G) {
                         : G.gs + (int)(((float)(q - 4 * G.gs) + 0.5f) * __builtin_amdgcn_rcpf((float)G.hp2));
 }
 
-__device__ __forceinline__ void cell_add(unsigned char* __restrict__ cells, int cell, int cshift, int copy,
-                                         const K1Px& p) {
-    // 32-bit LDS offset (a 64-bit pointer product costs a quarter-rate v_mad_u64_u32)
-    unsigned char* a = cells + __umul24((unsigned)((cell << cshift) | copy), (unsigned)kCellBytes);
-    atomicAdd(reinterpret_cast<unsigned long long*>(a), ((unsigned long long)p.hi << 32) | p.lo);
-    atomicAdd(reinterpret_cast<double*>(a + 8), p.h);
-    atomicAdd(reinterpret_cast<double*>(a + 16), p.s);
+// A thread's accumulator addresses: the LDS base, the copy shifts and its
+// copies (byte offsets are 32-bit: a 64-bit pointer product costs a
+// quarter-rate v_mad_u64_u32)
+struct Acc {
+    unsigned char* base;     // the count words at base, sum h at base + hsum, sum s soff further
+    int hsum, soff;
+    int cs, hs;
+    unsigned copy8, copyh8;  // this thread's copies x 8 bytes
+};
+
+__device__ __forceinline__ void acc_add(const Acc& A, int cell, int g, unsigned lo, unsigned hi, double h, double s) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(A.base + (((unsigned)cell << (A.cs + 3)) | A.copy8)),
+              ((unsigned long long)hi << 32) | lo);
+    unsigned char* ha = A.base + A.hsum + (((unsigned)g << (A.hs + 3)) | A.copyh8);
+    atomicAdd(reinterpret_cast<double*>(ha), h);
+    atomicAdd(reinterpret_cast<double*>(ha + A.soff), s);
 }
+__device__ __forceinline__ void acc_add(const Acc& A, const K1Px& p) { acc_add(A, p.cell, p.grp, p.lo, p.hi, p.h, p.s); }
 
 struct Mom {
     unsigned sr, sg, sb, qr, qg, qb;
@@ -123,6 +146,7 @@ struct Mom {
 // most of a wave's lanes on one address, where LDS atomics serialise).
 struct CellRun {
     int cell;            // -1: empty
+    int grp;
     unsigned lo, hi;
     double h, s;
 };
@@ -131,8 +155,7 @@ struct CellRun {
 // bit i of the result = pixel i deferred.
 template <bool TRI, bool SMALL, bool MERGE>
 __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
-                                             const unsigned char* __restrict__ code8,
-                                             unsigned char* __restrict__ cells, int cshift, int copy,
+                                             const unsigned char* __restrict__ code8, const Acc& A,
                                              const K1Grid& G, CellRun* run, unsigned& nsame) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
@@ -204,15 +227,11 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
                 run->h += p.h;
                 run->s += p.s;
             } else {
-                if (run->cell >= 0) {
-                    K1Px q;
-                    q.lo = run->lo; q.hi = run->hi; q.h = run->h; q.s = run->s;
-                    cell_add(cells, run->cell, cshift, copy, q);
-                }
-                *run = CellRun{p.cell, p.lo, p.hi, p.h, p.s};
+                if (run->cell >= 0) acc_add(A, run->cell, run->grp, run->lo, run->hi, run->h, run->s);
+                *run = CellRun{p.cell, p.grp, p.lo, p.hi, p.h, p.s};
             }
         } else {
-            cell_add(cells, p.cell, cshift, copy, p);
+            acc_add(A, p);
         }
         def |= p.dfr << i;
         // the vote sample: are all four pixels in one cell?  (every group
@@ -237,17 +256,22 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                                                long nitems, GridParams gp, K1Grid G,
                                                const ClassTables* __restrict__ tabs,
                                                const double* __restrict__ k255g, PaletteDev out, long a_stride,
-                                               long h_stride, int cshift) {
+                                               long h_stride, int cfg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x;
     const long it0 = (long)blockIdx.x * nitems / gridDim.x, it1 = (long)(blockIdx.x + 1) * nitems / gridDim.x;
     if (it0 >= it1) return;                                     // block-uniform
-    const int C = 1 << cshift, copy = tid & (C - 1);
+    const int cshift = k1_cs(cfg), hshift = k1_hs(cfg);
+    const int C = 1 << cshift, CH = 1 << hshift;
     constexpr int kT = KT, kG = kChunk / (4 * KT);              // threads; 4-pixel groups per thread per chunk
     static_assert(kG == 4 || kG == 8, "K1 tile");
     const int tl = gp.tl, ncell = G.ncell;
-    const LVar V = l_var(tl, ncell, cshift, code_bytes<TRI>());
+    const LVar V = l_var(tl, ncell, cfg, code_bytes<TRI>());
     unsigned char* cells = smem + V.cells;
+    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(cells);
+    double* hsum = reinterpret_cast<double*>(smem + V.hsum);
+    double* ssum = hsum + V.soff / 8;
+    const Acc A{cells, V.hsum, V.soff, cshift, hshift, (unsigned)(tid & (C - 1)) << 3, (unsigned)(tid & (CH - 1)) << 3};
     unsigned char* code8 = smem + V.code;
     double* k255 = reinterpret_cast<double*>(smem + V.k255);
     unsigned long long* red = reinterpret_cast<unsigned long long*>(smem + V.red);
@@ -260,7 +284,6 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
     unsigned* seg = reinterpret_cast<unsigned*>(smem + V.seg);
     unsigned* r255 = reinterpret_cast<unsigned*>(smem + V.r255);
     unsigned long long* rmx = reinterpret_cast<unsigned long long*>(smem + V.rmx);
-    double* gacc = reinterpret_cast<double*>(smem + V.gacc);
     {
         static_assert(code_bytes<TRI>() % 16 == 0, "uint4 copy");
         const uint4* src = reinterpret_cast<const uint4*>(TRI ? tabs->code_tri : tabs->code8);
@@ -268,7 +291,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         for (int i = tid; i < code_bytes<TRI>() / 16; i += kT) dst[i] = src[i];
         for (int i = tid; i < 256; i += kT) k255[i] = k255g[i];
         unsigned* z = reinterpret_cast<unsigned*>(smem);
-        for (int i = tid; i < V.code / 4; i += kT) z[i] = 0u;                        // cells
+        for (int i = tid; i < V.code / 4; i += kT) z[i] = 0u;                        // counts, h / s sums
         for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;           // run records
         if (tid < 2) vote[16 * tid] = 0u;
     }
@@ -325,7 +348,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             // (the prefetch's mask applied here, so nothing waits for it before the fold)
             unsigned a0 = p_ok ? p0 : 0u, a1 = p_ok ? p1 : 0u, a2 = p_ok ? p2 : 0u;
             if (!have_pf) ld(0, a0, a1, a2);
-            CellRun run{-1, 0u, 0u, 0.0, 0.0};
+            CellRun run{-1, 0, 0u, 0u, 0.0, 0.0};
             unsigned nsame = 0;                                   // this thread's groups in one cell
             auto loop = [&](auto mg) __attribute__((always_inline)) {
                 constexpr bool M = decltype(mg)::value;
@@ -334,17 +357,13 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                     // the next group (the last step reloads its own: unused)
                     unsigned n0, n1, n2;
                     const bool nok = ld_raw(st + 1 < kG ? st + 1 : st, n0, n1, n2);
-                    emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, cells, cshift, copy, G, &run, nsame)
+                    emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, A, G, &run, nsame)
                              << (4 * st);
                     a0 = nok ? n0 : 0u;
                     a1 = nok ? n1 : 0u;
                     a2 = nok ? n2 : 0u;
                 }
-                if (M && run.cell >= 0) {
-                    K1Px q;
-                    q.lo = run.lo; q.hi = run.hi; q.h = run.h; q.s = run.s;
-                    cell_add(cells, run.cell, cshift, copy, q);
-                }
+                if (M && run.cell >= 0) acc_add(A, run.cell, run.grp, run.lo, run.hi, run.h, run.s);
             };
             if (merge) loop(std::true_type{});
             else loop(std::false_type{});
@@ -364,7 +383,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                 K1Px px = k1_pixel<SMALL>(kr, kg, kb, kmx, kmn, kmx - kmn, code,
                                           k1_inv_pair(kmx - kmn > 1 ? kmx - kmn : 1, kmx > 1 ? kmx : 1), G);
                 if (px.cell == ncell) px = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
-                cell_add(cells, px.cell, cshift, copy, px);
+                acc_add(A, px);
             }
         }
         // deferred pixels (a non-special hue exactly on a half-bin boundary,
@@ -401,7 +420,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                     const int kr = q[0], kg = q[1], kb = q[2];
                     const int kmx = max(kr, max(kg, kb)), kmn = min(kr, min(kg, kb));
                     const K1Px px = k1_exact(kr, kg, kb, code8[code_idx<TRI>(kmx, kmx - kmn)], gp.Lh, k255, G);
-                    cell_add(cells, px.cell, cshift, copy, px);
+                    acc_add(A, px);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();                  // the queue is read before it is refilled
@@ -410,8 +429,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         }
         const long pad = base + kChunk - full_end;                // zero pixels of masked groups
         if (pad > 0 && tid == 0)
-            atomicAdd(reinterpret_cast<unsigned long long*>(cells + kCellBytes * (zcell << cshift)),
-                      (unsigned long long)(-pad));
+            atomicAdd(cnt + (zcell << cshift), (unsigned long long)(-pad));
         {
             // (c, img) are the next chunk's already; as ld(0) of that chunk
             // (unconditional: a load under a branch is waited for at the join)
@@ -430,7 +448,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         for (int q = tid; q <= ncell; q += kT) {
             unsigned long long v = 0;
             for (int k = 0; k < C; k++) {
-                unsigned long long* wp = reinterpret_cast<unsigned long long*>(cells + kCellBytes * ((q << cshift) + k));
+                unsigned long long* wp = cnt + ((q << cshift) + k);
                 v += *wp;
                 *wp = 0ull;
             }
@@ -465,22 +483,6 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             if (lane_id() == 0)
 #pragma unroll
                 for (int k = 0; k < 6; k++) red[wv * 8 + k] = m64[k];
-            // per-cell h and s sums (all copies) into the run's group sums
-            for (int q = tid; q <= ncell; q += kT) {
-                double h = 0.0, s = 0.0;
-                for (int k = 0; k < C; k++) {
-                    double* a = reinterpret_cast<double*>(cells + kCellBytes * ((q << cshift) + k) + 8);
-                    h += a[0];
-                    s += a[1];
-                    a[0] = 0.0;
-                    a[1] = 0.0;
-                }
-                if (q < ncell && (h != 0.0 || s != 0.0)) {
-                    const int g = group_of_cell(q, G);
-                    atomicAdd(&gacc[g], h);
-                    atomicAdd(&gacc[tl + g], s);
-                }
-            }
             __syncthreads();
             char* arec = reinterpret_cast<char*>(out.sums) + cimg * a_stride;   // image's A record base
             double* gsum = reinterpret_cast<double*>(reinterpret_cast<char*>(out.gsum) + cimg * a_stride);
@@ -495,15 +497,24 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                     const double sv = (double)(rmx[g] - 255ull * n255) * (1.0 / 255.0) + 0.999999 * (double)n255;
                     atomicAdd(&gsum[2 * tl + g], sv);
                 }
-                const double h = gacc[g], s = gacc[tl + g];
+                // the run's h / s sums of group g: its CH copies (one thread per group)
+                double h = 0.0, s = 0.0;
+                for (int k = 0; k < CH; k++) {
+                    h += hsum[(g << hshift) + k];
+                    s += ssum[(g << hshift) + k];
+                    hsum[(g << hshift) + k] = 0.0;
+                    ssum[(g << hshift) + k] = 0.0;
+                }
                 if (h != 0.0) atomicAdd(&gsum[g], h);
                 if (s != 0.0) atomicAdd(&gsum[tl + g], s);
                 sacc += s;
                 seg[g] = 0;
                 r255[g] = 0;
                 rmx[g] = 0;
-                gacc[g] = 0.0;
-                gacc[tl + g] = 0.0;
+            }
+            if (tid < CH) {                                       // the deferred pixels' dummy group
+                hsum[(tl << hshift) + tid] = 0.0;
+                ssum[(tl << hshift) + tid] = 0.0;
             }
             for (int q = tid; q < ncell; q += kT) {
                 const unsigned n = rcell[q];
@@ -533,13 +544,13 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
 template <int KT, bool TRI>
 void launch_form(int grid, size_t lds, hipStream_t st, const uint8_t* const* d_imgs, long npix, int nchunks,
                  long nitems, const GridParams& gp, const K1Grid& G, const ClassTables* tabs, const double* k255,
-                 const PaletteDev& out0, long a_stride, long h_stride, int cshift) {
+                 const PaletteDev& out0, long a_stride, long h_stride, int cfg) {
     if (G.small_c)
         phd_launch((k_k1t<KT, TRI, true>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs,
-                   k255, out0, a_stride, h_stride, cshift);
+                   k255, out0, a_stride, h_stride, cfg);
     else
         phd_launch((k_k1t<KT, TRI, false>), dim3(grid), dim3(KT), lds, st, d_imgs, npix, nchunks, nitems, gp, G,
-                   tabs, k255, out0, a_stride, h_stride, cshift);
+                   tabs, k255, out0, a_stride, h_stride, cfg);
 }
 
 constexpr int kLds1 = 158 * 1024;   // one block per CU
@@ -547,33 +558,53 @@ constexpr int kLds2 = 79 * 1024;    // two blocks per CU
 
 }  // namespace
 
-// copies (log2) of the one-block form, -1 when it does not fit: the full code
-// table, else (fine grids: 36/4/5's 3312 hue cells) the triangular one
-static int cshift_full(const GridParams& gp) {
-    const int ncell = HueCells::count(gp);
-    for (int cs = 3; cs >= 0; cs--)
-        if (l_var(gp.tl, ncell, cs, code_bytes<false>()).end <= kLds1) return cs;
-    return -1;
-}
-static int cshift_tri1(const GridParams& gp) {
-    const int ncell = HueCells::count(gp);
-    for (int cs = 3; cs >= 0; cs--)
-        if (l_var(gp.tl, ncell, cs, code_bytes<true>()).end <= kLds1) return cs;
-    return -1;
+// Expected LDS cycles of one 16-lane group's 64-bit atomic into an array of
+// (slots x 2^k lane copies), copy = lane & (2^k - 1), slots random: the lanes
+// of one copy spread over 16 / 2^k bank pairs, the group takes the largest
+// pile (16 copies: one cycle, conflict-free).
+static double k1_conflicts(int k) {
+    static const double e[5] = {3.3, 3.1, 2.5, 2.0, 1.0};
+    return e[k < 0 ? 0 : (k > 4 ? 4 : k)];
 }
 
+// The accumulator layout (k1_cfg: count-word and h / s copy shifts) of least
+// expected conflict cost -- one count atomic and two h / s atomics per pixel --
+// that fits `lds` bytes with code table `code_bytes`, or -1.  At least
+// 2^cs_min count copies (flat images put many lanes on one cell).
+static int k1_config(const GridParams& gp, int code_bytes, int lds, int cs_min) {
+    const int ncell = HueCells::count(gp);
+    int best = -1;
+    double bc = 1e30;
+    for (int cs = 3; cs >= cs_min; cs--)
+        for (int hs = 4; hs >= 0; hs--) {
+            const int cfg = k1_cfg(cs, hs);
+            if (l_var(gp.tl, ncell, cfg, code_bytes).end > lds) continue;
+            const double c = k1_conflicts(cs) + 2.0 * k1_conflicts(hs);
+            if (c < bc - 1e-9) {
+                bc = c;
+                best = cfg;
+            }
+        }
+    return best;
+}
+
+// the one-block form's layouts: the full code table, and the triangular one
+// (fine grids: 36/4/5's 3312 hue cells only fit with it)
+static int cfg_full(const GridParams& gp) { return k1_config(gp, code_bytes<false>(), kLds1, 0); }
+static int cfg_tri1(const GridParams& gp) { return k1_config(gp, code_bytes<true>(), kLds1, 0); }
+static double cfg_cost(int cfg) { return cfg < 0 ? 1e30 : k1_conflicts(k1_cs(cfg)) + 2.0 * k1_conflicts(k1_hs(cfg)); }
+
+// >= 0 when the table K1 runs this grid (a k1_cfg of the one-block form)
 int k1t_cshift(const GridParams& gp, const ClassTables& t) {
     if (!t.codes_ok) return -1;
-    return std::max(cshift_full(gp), cshift_tri1(gp));
+    return std::max(cfg_full(gp), cfg_tri1(gp));
 }
 
-// copies (log2) of the two-block form (triangular code table), -1 when it does not fit
+// the two-block form's layout (triangular code table, >= 2 count copies), -1
+// when it does not fit
 int k1t_cshift2(const GridParams& gp, const ClassTables& t) {
     if (!t.codes_ok) return -1;
-    const int ncell = HueCells::count(gp);
-    for (int cs = 3; cs >= 1; cs--)                       // >= 2 lane copies
-        if (l_var(gp.tl, ncell, cs, code_bytes<true>()).end <= kLds2) return cs;
-    return -1;
+    return k1_config(gp, code_bytes<true>(), kLds2, 1);
 }
 
 hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int width, const GridParams& gp,
@@ -602,7 +633,7 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     const long cus = num_cus();
     const bool two = cshift2 >= 0 && 19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus);
     if (two) {                                            // two 512-thread blocks per CU
-        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;
+        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;   // (a k1_cfg)
         // on a call split over two lanes, one block per CU: the other half of
         // each CU stays free for the other lane's FFT blocks (k1_blocks_per_cu)
         const int grid = (int)std::min<long>(nitems, (long)k1_blocks_per_cu() * cus);
@@ -610,18 +641,19 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
                                h_stride, cshift2);
     } else {                                              // one 1024-thread block per CU
         const int grid = (int)std::min<long>(nitems, cus);
-        // the triangular code table leaves 31 KiB more for lane copies of the
-        // cells (fine grids: 36/4/5's 3312 hue cells only fit with it)
-        const int cs_full = cshift_full(gp), cs_tri = cshift_tri1(gp);
-        if (cs_tri < 0 && cs_full < 0) return hipErrorInvalidValue;   // k1t_cshift said no
-        if (cs_tri > cs_full) {
-            const size_t lds = (size_t)l_var(gp.tl, ncell, cs_tri, code_bytes<true>()).end;
+        // the triangular code table leaves 31 KiB more for the accumulators'
+        // lane copies (fine grids: 36/4/5's 3312 hue cells only fit with it);
+        // the full table where its layout is as good
+        const int c_full = cfg_full(gp), c_tri = cfg_tri1(gp);
+        if (c_tri < 0 && c_full < 0) return hipErrorInvalidValue;   // k1t_cshift said no
+        if (cfg_cost(c_tri) < cfg_cost(c_full) - 1e-9) {
+            const size_t lds = (size_t)l_var(gp.tl, ncell, c_tri, code_bytes<true>()).end;
             launch_form<1024, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0, a_stride,
-                                    h_stride, cs_tri);
+                                    h_stride, c_tri);
         } else {
-            const size_t lds = (size_t)l_var(gp.tl, ncell, cs_full, code_bytes<false>()).end;
+            const size_t lds = (size_t)l_var(gp.tl, ncell, c_full, code_bytes<false>()).end;
             launch_form<1024, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
-                                     a_stride, h_stride, cs_full);
+                                     a_stride, h_stride, c_full);
         }
     }
     return hipGetLastError();
@@ -657,6 +689,9 @@ int k1_host_pixels(const GridParams& gp, const ClassTables& t, const uint8_t* rg
                            : k1_pixel_x<false>(X, special, kmx, kmn, kd, code, e, G);
         const bool def = p.cell == G.ncell;
         if (def) p = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
+        // the group the kernel's h / s atomics use must be the cell's (HueCells)
+        const int want_g = p.cell < 4 * G.gs ? p.cell >> 2 : G.gs + (p.cell - 4 * G.gs) / G.hp2;
+        if (p.grp != want_g) return -3;
         cell[i] = p.cell;
         h[i] = p.h;
         s[i] = p.s;

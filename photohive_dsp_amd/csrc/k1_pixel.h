@@ -47,6 +47,8 @@ struct K1Grid {
     int gray_cb;     // cgs - 2 hp spvp: gray / black cell base (code >= spvp)
     int gs;          // gray_start: first gray / black group
     int ncell;       // HueCells::count; cell ncell is the dummy of deferred pixels
+    int tl;          // groups; group tl is the dummy of deferred pixels (K1's per-group h / s sums)
+    int gmg;         // gs - spvp: a gray / black code's group is code + gmg
     int small_c;     // every c < 64: the boundary properties are bit masks
     unsigned long long below_m;   // bit c: an exact boundary hue at B_c counts below it
     unsigned long long defer_m;   // bit c: B_c is not a multiple of 60 (onb pixels defer)
@@ -111,6 +113,8 @@ K1_HD void k1_grid_init(K1Grid& G, const GridParams& g) {
     G.gs = g.tl - g.ng - 1;
     G.gray_cb = 4 * G.gs - G.hp2 * G.spvp;
     G.ncell = 4 * G.gs + (g.ng + 1) * 2 * g.hp;
+    G.tl = g.tl;
+    G.gmg = G.gs - G.spvp;
     // c < 720 / Lh (X < 6 kd)
     G.small_c = (720 + G.lh - 1) / G.lh <= 64;
     G.below_m = G.defer_m = 0ull;
@@ -138,6 +142,7 @@ K1_HD int k1_halfbin(int n2, float rkd, const K1Grid& G) {
 
 struct K1Px {
     int cell;        // ncell when deferred
+    int grp;         // the cell's group (arm_octree's), tl when deferred
     unsigned dfr;    // 1 when deferred
     unsigned lo, hi; // the cell word: lo = 1 | (kmax == 255) << 16, hi = kmax
     double h, s;
@@ -227,8 +232,11 @@ K1_HD K1Px k1_pixel_x(int X, bool special, int kmx, int kmn, int kd, int code, c
     const int mul = color ? 4 : G.hp2;
     const int add = color ? k1_mul(c >> 1, G.ac) + 1 : G.gray_cb;
     const int cell = k1_mul(code, mul) + add + c - (int)below;
+    // its group: colour (c / 2) spvp + code (= cell / 4), gray / black code + gs - spvp
+    const int grp = color ? k1_mul(c >> 1, G.spvp) + code : code + G.gmg;
     K1Px p;
     p.cell = def ? G.ncell : cell;
+    p.grp = def ? G.tl : grp;
     p.dfr = def;
     p.lo = 1u + ((unsigned)((kmx + 1) >> 8) << 16);
     p.hi = (unsigned)kmx;
@@ -292,8 +300,10 @@ K1_HD K1Px k1_exact(int kr, int kg, int kb, int code, double Lh, const double* k
     if (code < G.spvp) {
         const int hi = (int)(h / Lh);
         const int l = cg - 2 * hi + 1;
-        p.cell = 4 * (hi * G.spvp + code) + (l < 0 ? 0 : (l > 3 ? 3 : l));
+        p.grp = hi * G.spvp + code;
+        p.cell = 4 * p.grp + (l < 0 ? 0 : (l > 3 ? 3 : l));
     } else {
+        p.grp = code + G.gmg;
         p.cell = G.gray_cb + code * G.hp2 + cg;
     }
     p.dfr = 0u;

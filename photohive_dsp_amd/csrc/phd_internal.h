@@ -76,8 +76,8 @@ struct GridParams {
 struct FastCls {
     int lh;                    // Lh = 360 / h_partitions (integer division, :41)
     int use_thr;               // Si from ClsEnt::thr (s_partitions <= 6), else si8 in global memory
-    int k1t_cshift = -1;       // the table K1 (k1.hip) fits this grid with 1 << k1t_cshift copies
-    int k1t_cshift2 = -1;      // ... as two 512-thread blocks per CU (triangular code table), else -1
+    int k1t_cshift = -1;       // >= 0: the table K1 (k1.hip) runs this grid (its accumulator layout, k1_cfg)
+    int k1t_cshift2 = -1;      // ... as two 512-thread blocks per CU (triangular code table): its layout, else -1
 };
 // Si is non-decreasing in kd = kmax - kmin for a fixed kmax (s = d / max is), so
 // it is -1 plus the number of thresholds kd reaches.

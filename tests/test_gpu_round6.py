@@ -51,7 +51,8 @@ def test_legacy_entry_members_freed_by_caller():
     from photohive_dsp_amd.utils import pil_image_to_image_rgb
     from PIL import Image
     img = synth.make("structured", 384, 512, 77)
-    im = pil_image_to_image_rgb(Image.fromarray(img))
+    pil = Image.fromarray(img)                       # owns the planes (utils.py keeps them on it)
+    im = pil_image_to_image_rgb(pil)
     ptr = L.lib.get_full_report_data(ctypes.byref(im), None, 18, 2, 3, 0.1, 0.1, 0.95, 1000, 1, 40, 72,
                                      0.1, 0.9, 1.20, 0.3, 2)
     assert ptr, L.last_error()

@@ -6,6 +6,7 @@ mkdir -p gpurun_out
 for step in "$@"; do
   name="${step%%:*}"; rest="${step#*:}"; secs="${rest%%:*}"; cmd="${rest#*:}"
   echo "=== $name ($secs s): $cmd"
+  mkdir -p "$(dirname "gpurun_out/$name.log")"
   timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
   rc=$?
   echo "=== $name rc=$rc"
