@@ -335,6 +335,8 @@ struct ColK {
     // waves per SIMD of the launch bounds: sized for two resident blocks per
     // CU, one when the column and twiddles fill the LDS
     static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
+    // (round 6: 3000 rows at 320 threads, three passes, needs three waves per
+    // SIMD for two blocks, i.e. 168 VGPRs: 50-60 spilled; not pursued)
     static constexpr int MINW = (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2;
     // The next column streams into the column buffer by LDS-DMA (no
     // registers) while the current one finishes (round 5).

@@ -295,8 +295,16 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(640, 128, 5, 8, 16)        \
     X(480, 128, 5, 6, 16)        \
     X(512, 64, 8, 8, 8)
+// (the 3000-row plan's threads and radices are overridable for A/B builds:
+// make variant VFLAGS='-DPHD_C3000_T=320 "-DPHD_C3000_R=20, 15, 10"')
+#ifndef PHD_C3000_T
+#define PHD_C3000_T 256
+#endif
+#ifndef PHD_C3000_R
+#define PHD_C3000_R 15, 10, 20
+#endif
 #define PHD_CT_COLS(X)           \
-    X(3000, 256, 15, 10, 20)     \
+    X(3000, PHD_C3000_T, PHD_C3000_R) \
     X(6000, 512, 15, 20, 20)     \
     X(4000, 256, 10, 20, 20)     \
     X(2000, 256, 10, 10, 20)     \
