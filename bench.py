@@ -904,7 +904,7 @@ def main(argv=None):
         else:
             dist.init_process_group(backend)
     cx = Ctx(args, world, rank, backend, dev)
-    if os.environ.get("PHD_BENCH_MAPS"):
+    if os.environ.get("PHD_BENCH_MAPS") and hasattr(cx.lib, "phd_install_crash_maps"):
         # the mappings AT a fault (SIGSEGV / SIGABRT ...), written by the library's handler
         cx.lib.phd_install_crash_maps(f"{os.environ['PHD_BENCH_MAPS']}.fault".encode())
     dump_maps("ctx")
@@ -1002,7 +1002,8 @@ def main(argv=None):
         print(json.dumps(line), flush=True)
     # the library's explicit teardown (threads joined, HIP resources released)
     # before torch's and HIP's own exit handlers; it would also run at exit
-    cx.lib.phd_shutdown()
+    if hasattr(cx.lib, "phd_shutdown"):                  # (older builds in A/B runs lack it)
+        cx.lib.phd_shutdown()
     if world > 1:
         torch.distributed.destroy_process_group()
     return 0

@@ -128,14 +128,19 @@ lib.free_full_report.argtypes = [P(P(Full_Report_Data))]
 lib.phd_free_reports.restype = None
 lib.phd_free_reports.argtypes = [P(P(Full_Report_Data)), ctypes.c_int]
 lib.phd_free_pgm.argtypes = [P(Image_PGM)]
-lib.phd_shutdown.restype = None
-lib.phd_shutdown.argtypes = []
-lib.phd_install_crash_maps.restype = ctypes.c_int
-lib.phd_install_crash_maps.argtypes = [ctypes.c_char_p]
-lib.phd_debug_library_threads.restype = ctypes.c_int
-lib.phd_debug_library_threads.argtypes = [ctypes.c_int]
-lib.phd_debug_legacy_report.restype = P(Full_Report_Data)
-lib.phd_debug_legacy_report.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+# round-6 entry points, bound only when present: an A/B timing run may load an
+# older build through PHD_LIB (tools/); the shipped library exports all of them
+# (tests/test_abi.py checks every symbol of include/photohive_dsp.h)
+for _name, _res, _args in (("phd_shutdown", None, []),
+                           ("phd_install_crash_maps", ctypes.c_int, [ctypes.c_char_p]),
+                           ("phd_debug_library_threads", ctypes.c_int, [ctypes.c_int]),
+                           ("phd_debug_legacy_report", P(Full_Report_Data),
+                            [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int])):
+    try:
+        _f = getattr(lib, _name)
+    except AttributeError:
+        continue
+    _f.restype, _f.argtypes = _res, _args
 lib.phd_last_error.restype = ctypes.c_char_p
 lib.phd_device_info.restype = ctypes.c_int
 lib.phd_device_info.argtypes = [ctypes.c_char_p, ctypes.c_int]
