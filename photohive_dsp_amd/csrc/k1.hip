@@ -195,15 +195,20 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
         const int q = i & 1, sh = 16 * (i >> 1);           // pixel i: pair q, half i >> 1
         code[i] = code8[(Ix[q] >> sh) & 0xFFFF];
     }
+    // the reciprocal's operands of both pixels of a pair in u16 lanes:
+    // max(kd, 1) max(kmx, 1) <= 65025
+    const u16x2 km02 = __builtin_elementwise_max(mx02, one), km13 = __builtin_elementwise_max(mx13, one);
+    const unsigned Pp[2] = {as1(__builtin_elementwise_max(kd02, one) * km02),
+                            as1(__builtin_elementwise_max(kd13, one) * km13)};
+    const unsigned Km[2] = {as1(km02), as1(km13)};
     K1Inv ekd[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int q = i & 1, sh = 16 * (i >> 1);
-        const int kmx = (Mx[q] >> sh) & 0xFFFF, kd = (Kd[q] >> sh) & 0xFFFF;
         // from the VALU (round 4: an LDS table of reciprocals measured slower,
         // 46 against 40 us per image -- the LDS is the busier pipe); one
         // reciprocal of kd kmax per pixel since round 6
-        ekd[i] = k1_inv_pair(kd > 1 ? kd : 1, kmx > 1 ? kmx : 1);
+        ekd[i] = k1_inv_p((Pp[q] >> sh) & 0xFFFF, (Km[q] >> sh) & 0xFFFF);
     }
     // X of both pixels of each pair in 16-bit lanes (k1_x_pair)
     const unsigned Xp[2] = {as1(k1_x_pair(r02, g02, b02, mx02, kd02)), as1(k1_x_pair(r13, g13, b13, mx13, kd13))};

@@ -76,8 +76,7 @@ struct K1Inv {
     float rkd;       // 1 / kd1 in fp32: <= 1.5 ulp on the device, 1 ulp on the host
     unsigned pad;
 };
-K1_HD K1Inv k1_inv_pair(int kd1, int km1) {
-    const int p = k1_mul(kd1, km1);
+K1_HD K1Inv k1_inv_p(int p, int km1) {      // p = kd1 km1 (the kernel forms it for a u16 pair at once)
     const float pf = (float)p;
 #if defined(__HIP_DEVICE_COMPILE__)
     const float r = __builtin_amdgcn_rcpf(pf);
@@ -91,6 +90,7 @@ K1_HD K1Inv k1_inv_pair(int kd1, int km1) {
     const double d = (double)r;
     return K1Inv{std::fma(d, (double)e, d), (float)km1 * r, 0u};
 }
+K1_HD K1Inv k1_inv_pair(int kd1, int km1) { return k1_inv_p(k1_mul(kd1, km1), km1); }
 
 // q - floor(q) for 0 <= q < 2^23 (exact in fp32)
 K1_HD float k1_fract(float q, int c) {
