@@ -329,6 +329,9 @@ def pmc_traffic(args, H, W):
         return None, None
     src = (f"{os.path.relpath(args.pmc, ROOT)}: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
            "config (tools/pmc_collect.py), not measured in this run")
+    if pm.get("bench_args"):
+        src += (f"; profiled run: bench.py {' '.join(pm['bench_args'])}"
+                + (f", {pm['images_profiled']} images" if pm.get("images_profiled") else ""))
     if pm.get("calibration"):
         src += f"; FETCH_SIZE x each kernel's fetch_factor, calibrated on its algorithmic bytes ({pm['calibration']})"
     return pm["kernels"], src
