@@ -199,6 +199,10 @@ def _throughput(h, w, procs, per, seed0):
         start_at = time.time() + 5.0 + 0.2 * procs
         jobs = [("O2", h, w, [seed0 + per * p + k for k in range(per)], start_at, 1) for p in range(procs)]
         res = pool.map(_cpu_worker, jobs, chunksize=1)
+        # the workers exit on their own (the with-block's terminate() would
+        # SIGTERM them, which a profiler wrapping the run reports per process)
+        pool.close()
+        pool.join()
     return sum(r[0] for r in res), max(r[2] for r in res) - min(r[1] for r in res)
 
 
