@@ -90,9 +90,9 @@ __host__ __device__ inline int k1_cs(int cfg) { return cfg & 15; }
 __host__ __device__ inline int k1_hs(int cfg) { return cfg >> 4; }
 
 struct LVar {
-    int cells, hsum, soff, code, k255, red, dq, rcell, cg, seg, r255, rmx, end;
+    int cells, hsum, soff, code, k255, red, dq, rcell, cg, seg, r255, rmx, ctab, end;
 };
-__host__ __device__ inline LVar l_var(int tl, int ncell, int cfg, int code_bytes) {
+__host__ __device__ inline LVar l_var(int tl, int ncell, int cfg, int code_bytes, int ncodes) {
     LVar v;
     v.cells = 0;                                                    // (ncell + 1) << cs u64 count words
     v.hsum = (8 * ((ncell + 1) << k1_cs(cfg)) + 15) & ~15;          // (tl + 1) << hs f64 sum h, then sum s
@@ -106,7 +106,8 @@ __host__ __device__ inline LVar l_var(int tl, int ncell, int cfg, int code_bytes
     v.seg = v.cg + 4 * tl;                                          // tl u32: the run's group counts
     v.r255 = v.seg + 4 * tl;                                        // tl u32: the run's #(kmax == 255)
     v.rmx = (v.r255 + 4 * tl + 7) & ~7;                             // tl u64: the run's sum kmax
-    v.end = v.rmx + 8 * tl;
+    v.ctab = v.rmx + 8 * tl;                                        // ncodes K1Code: cell / group terms
+    v.end = v.ctab + 8 * ncodes;
     return v;
 }
 
@@ -155,7 +156,8 @@ struct CellRun {
 // bit i of the result = pixel i deferred.
 template <bool TRI, bool SMALL, bool MERGE>
 __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned w2, Mom& m,
-                                             const unsigned char* __restrict__ code8, const Acc& A,
+                                             const unsigned char* __restrict__ code8,
+                                             const K1Code* __restrict__ ctab, const Acc& A,
                                              const K1Grid& G, CellRun* run, unsigned& nsame) {
     const u16x2 one = {1, 1};
     const u16x2 r02 = as2(__builtin_amdgcn_perm(w1, w0, 0x0c060c00u));
@@ -224,7 +226,8 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
             const int kr = (R[q] >> sh) & 0xFFFF, kg = (Gc[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
             special = (kr == kg) | (kg == kb) | (kr == kb);
         }
-        const K1Px p = k1_pixel_x<SMALL>((int)((Xp[q] >> sh) & 0xFFFF), special, kmx, kmn, kd, code[i], ekd[i], G);
+        const K1Px p = k1_pixel_x<SMALL>((int)((Xp[q] >> sh) & 0xFFFF), special, kmx, kmn, kd, ctab[code[i]], ekd[i],
+                                         G);
         if constexpr (MERGE) {
             if (p.cell == run->cell) {
                 run->lo += p.lo;
@@ -271,7 +274,9 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
     constexpr int kT = KT, kG = kChunk / (4 * KT);              // threads; 4-pixel groups per thread per chunk
     static_assert(kG == 4 || kG == 8, "K1 tile");
     const int tl = gp.tl, ncell = G.ncell;
-    const LVar V = l_var(tl, ncell, cfg, code_bytes<TRI>());
+    const int ncodes = k1_ncodes(G);
+    const LVar V = l_var(tl, ncell, cfg, code_bytes<TRI>(), ncodes);
+    K1Code* ctab = reinterpret_cast<K1Code*>(smem + V.ctab);
     unsigned char* cells = smem + V.cells;
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(cells);
     double* hsum = reinterpret_cast<double*>(smem + V.hsum);
@@ -295,9 +300,10 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         uint4* dst = reinterpret_cast<uint4*>(code8);
         for (int i = tid; i < code_bytes<TRI>() / 16; i += kT) dst[i] = src[i];
         for (int i = tid; i < 256; i += kT) k255[i] = k255g[i];
+        for (int i = tid; i < ncodes; i += kT) ctab[i] = k1_code_entry(G, i);
         unsigned* z = reinterpret_cast<unsigned*>(smem);
         for (int i = tid; i < V.code / 4; i += kT) z[i] = 0u;                        // counts, h / s sums
-        for (int i = V.rcell / 4 + tid; i < V.end / 4; i += kT) z[i] = 0u;           // run records
+        for (int i = V.rcell / 4 + tid; i < V.ctab / 4; i += kT) z[i] = 0u;          // run records
         if (tid < 2) vote[16 * tid] = 0u;
     }
     // the (0, 0, 0) pixel's cell: masked groups past the image end are zero
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
                     // the next group (the last step reloads its own: unused)
                     unsigned n0, n1, n2;
                     const bool nok = ld_raw(st + 1 < kG ? st + 1 : st, n0, n1, n2);
-                    emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, A, G, &run, nsame)
+                    emask |= k1_group<TRI, SMALL, M>(a0, a1, a2, m, code8, ctab, A, G, &run, nsame)
                              << (4 * st);
                     a0 = nok ? n0 : 0u;
                     a1 = nok ? n1 : 0u;
@@ -583,7 +589,7 @@ static int k1_config(const GridParams& gp, int code_bytes, int lds, int cs_min) 
     for (int cs = 3; cs >= cs_min; cs--)
         for (int hs = 4; hs >= 0; hs--) {
             const int cfg = k1_cfg(cs, hs);
-            if (l_var(gp.tl, ncell, cfg, code_bytes).end > lds) continue;
+            if (l_var(gp.tl, ncell, cfg, code_bytes, gp.sp * gp.vp + gp.ng + 1).end > lds) continue;
             const double c = k1_conflicts(cs) + 2.0 * k1_conflicts(hs);
             if (c < bc - 1e-9) {
                 bc = c;
@@ -638,7 +644,7 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
     const long cus = num_cus();
     const bool two = cshift2 >= 0 && 19 * ((nitems + 2 * cus - 1) / (2 * cus)) < 10 * ((nitems + cus - 1) / cus);
     if (two) {                                            // two 512-thread blocks per CU
-        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>()).end;   // (a k1_cfg)
+        const size_t lds = (size_t)l_var(gp.tl, ncell, cshift2, code_bytes<true>(), k1_ncodes(G)).end;   // (a k1_cfg)
         // on a call split over two lanes, one block per CU: the other half of
         // each CU stays free for the other lane's FFT blocks (k1_blocks_per_cu)
         const int grid = (int)std::min<long>(nitems, (long)k1_blocks_per_cu() * cus);
@@ -652,11 +658,11 @@ hipError_t launch_k1t_batch(const uint8_t* const* d_imgs, int n, int height, int
         const int c_full = cfg_full(gp), c_tri = cfg_tri1(gp);
         if (c_tri < 0 && c_full < 0) return hipErrorInvalidValue;   // k1t_cshift said no
         if (cfg_cost(c_tri) < cfg_cost(c_full) - 1e-9) {
-            const size_t lds = (size_t)l_var(gp.tl, ncell, c_tri, code_bytes<true>()).end;
+            const size_t lds = (size_t)l_var(gp.tl, ncell, c_tri, code_bytes<true>(), k1_ncodes(G)).end;
             launch_form<1024, true>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0, a_stride,
                                     h_stride, c_tri);
         } else {
-            const size_t lds = (size_t)l_var(gp.tl, ncell, c_full, code_bytes<false>()).end;
+            const size_t lds = (size_t)l_var(gp.tl, ncell, c_full, code_bytes<false>(), k1_ncodes(G)).end;
             launch_form<1024, false>(grid, lds, st, d_imgs, npix, nchunks, nitems, gp, G, tabs, k255, out0,
                                      a_stride, h_stride, c_full);
         }
@@ -690,8 +696,9 @@ int k1_host_pixels(const GridParams& gp, const ClassTables& t, const uint8_t* rg
         if (x2[0] != k1_x_pair((k1_u16x2){(unsigned short)kg, 0}, (k1_u16x2){(unsigned short)kb, 0},
                                (k1_u16x2){(unsigned short)kr, 0}, m2, d2)[0])
             return -2;                                   // the two lanes of a pair disagree
-        K1Px p = G.small_c ? k1_pixel_x<true>(X, special, kmx, kmn, kd, code, e, G)
-                           : k1_pixel_x<false>(X, special, kmx, kmn, kd, code, e, G);
+        const K1Code ce = k1_code_entry(G, code);
+        K1Px p = G.small_c ? k1_pixel_x<true>(X, special, kmx, kmn, kd, ce, e, G)
+                           : k1_pixel_x<false>(X, special, kmx, kmn, kd, ce, e, G);
         const bool def = p.cell == G.ncell;
         if (def) p = k1_exact(kr, kg, kb, code, gp.Lh, k255, G);
         // the group the kernel's h / s atomics use must be the cell's (HueCells)

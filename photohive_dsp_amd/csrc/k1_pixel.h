@@ -148,6 +148,33 @@ struct K1Px {
     double h, s;
 };
 
+// What a code contributes to its pixel's hue cell and group (round 6: read per
+// pixel from a small LDS table, code-indexed, instead of selecting between the
+// colour and the gray / black formulas): cell = a + m (c / 2) + c - below,
+// group = g0 + mg (c / 2).  Colour code: a = 4 code + 1, m = 4 spvp - 2, g0 =
+// code, mg = spvp (cell = 4 (hi spvp + code) + 1 + c - 2 hi - below); gray /
+// black code: a = gray_cb + code 2 hp, g0 = code + gs - spvp, m = mg = 0.
+struct K1Code {
+    short a, m, g0, mg;
+};
+K1_HD K1Code k1_code_entry(const K1Grid& G, int code) {
+    K1Code e;
+    if (code < G.spvp) {
+        e.a = (short)(4 * code + 1);
+        e.m = (short)G.ac;
+        e.g0 = (short)code;
+        e.mg = (short)G.spvp;
+    } else {
+        e.a = (short)(G.gray_cb + code * G.hp2);
+        e.m = 0;
+        e.g0 = (short)(code + G.gmg);
+        e.mg = 0;
+    }
+    return e;
+}
+// codes of a grid: spvp colour codes, then the gray groups and black
+K1_HD int k1_ncodes(const K1Grid& G) { return G.spvp + G.tl - G.gs; }
+
 typedef unsigned short k1_u16x2 __attribute__((ext_vector_type(2)));
 typedef short k1_i16x2 __attribute__((ext_vector_type(2)));
 
@@ -207,7 +234,7 @@ K1_HD k1_u16x2 k1_x_pair(k1_u16x2 r, k1_u16x2 g, k1_u16x2 b, k1_u16x2 mx, k1_u16
 // k1_pixel_x takes X from k1_x_pair (the kernel) and `special` (two channels
 // equal; read only by the !SMALL form); k1_pixel computes both itself.
 template <bool SMALL>   // SMALL == G.small_c
-K1_HD K1Px k1_pixel_x(int X, bool special, int kmx, int kmn, int kd, int code, const K1Inv& e,
+K1_HD K1Px k1_pixel_x(int X, bool special, int kmx, int kmn, int kd, const K1Code& ce, const K1Inv& e,
                       const K1Grid& G) {
     const int km1 = kmx > 1 ? kmx : 1;
     const float thr2 = G.rlh2 * e.rkd;                          // u / 2
@@ -227,13 +254,12 @@ K1_HD K1Px k1_pixel_x(int X, bool special, int kmx, int kmn, int kd, int code, c
         below = onb && special && ch >= 0 && ((ch & 1) || ch == 0);
         def = onb && !special;
     }
-    const bool color = code < G.spvp;
     // colour: 4 (hi spvp + code) + 1 + (c - 2 hi); gray / black: 4 gs + j 2 hp + c
-    const int mul = color ? 4 : G.hp2;
-    const int add = color ? k1_mul(c >> 1, G.ac) + 1 : G.gray_cb;
-    const int cell = k1_mul(code, mul) + add + c - (int)below;
-    // its group: colour (c / 2) spvp + code (= cell / 4), gray / black code + gs - spvp
-    const int grp = color ? k1_mul(c >> 1, G.spvp) + code : code + G.gmg;
+    // (K1Code); its group: colour (c / 2) spvp + code (= cell / 4), gray /
+    // black code + gs - spvp
+    const int hi = c >> 1;
+    const int cell = (int)ce.a + k1_mul(ce.m, hi) + c - (int)below;
+    const int grp = (int)ce.g0 + k1_mul(ce.mg, hi);
     K1Px p;
     p.cell = def ? G.ncell : cell;
     p.grp = def ? G.tl : grp;
@@ -257,7 +283,7 @@ K1_HD K1Px k1_pixel(int kr, int kg, int kb, int kmx, int kmn, int kd, int code, 
     const int xr = kg - kb + (kg < kb ? k1_mul(6, kd) : 0);
     const int X = isr ? xr : xs;
     const bool special = (kr == kg) | (kg == kb) | (kr == kb);
-    return k1_pixel_x<SMALL>(X, special, kmx, kmn, kd, code, e, G);
+    return k1_pixel_x<SMALL>(X, special, kmx, kmn, kd, k1_code_entry(G, code), e, G);
 }
 
 // A deferred pixel: rgb2hsv's double hue (the reference's expression on the
