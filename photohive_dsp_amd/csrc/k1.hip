@@ -212,6 +212,12 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
         // reciprocal of kd kmax per pixel since round 6
         ekd[i] = k1_inv_p((Pp[q] >> sh) & 0xFFFF, (Km[q] >> sh) & 0xFFFF);
     }
+    // the codes' cell / group terms, all four read before this group's
+    // atomics (LDS operations complete in order: a read issued after an atomic
+    // would wait for it)
+    K1Code ce[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) ce[i] = ctab[code[i]];
     // X of both pixels of each pair in 16-bit lanes (k1_x_pair)
     const unsigned Xp[2] = {as1(k1_x_pair(r02, g02, b02, mx02, kd02)), as1(k1_x_pair(r13, g13, b13, mx13, kd13))};
     unsigned def = 0;
@@ -226,8 +232,7 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
             const int kr = (R[q] >> sh) & 0xFFFF, kg = (Gc[q] >> sh) & 0xFFFF, kb = (B[q] >> sh) & 0xFFFF;
             special = (kr == kg) | (kg == kb) | (kr == kb);
         }
-        const K1Px p = k1_pixel_x<SMALL>((int)((Xp[q] >> sh) & 0xFFFF), special, kmx, kmn, kd, ctab[code[i]], ekd[i],
-                                         G);
+        const K1Px p = k1_pixel_x<SMALL>((int)((Xp[q] >> sh) & 0xFFFF), special, kmx, kmn, kd, ce[i], ekd[i], G);
         if constexpr (MERGE) {
             if (p.cell == run->cell) {
                 run->lo += p.lo;

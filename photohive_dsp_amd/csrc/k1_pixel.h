@@ -155,19 +155,19 @@ struct K1Px {
 // code, mg = spvp (cell = 4 (hi spvp + code) + 1 + c - 2 hi - below); gray /
 // black code: a = gray_cb + code 2 hp, g0 = code + gs - spvp, m = mg = 0.
 struct K1Code {
-    short a, m, g0, mg;
+    unsigned short a, m, g0, mg;   // all non-negative (ncell < 2^16: codes_ok grids)
 };
 K1_HD K1Code k1_code_entry(const K1Grid& G, int code) {
     K1Code e;
     if (code < G.spvp) {
-        e.a = (short)(4 * code + 1);
-        e.m = (short)G.ac;
-        e.g0 = (short)code;
-        e.mg = (short)G.spvp;
+        e.a = (unsigned short)(4 * code + 1);
+        e.m = (unsigned short)G.ac;
+        e.g0 = (unsigned short)code;
+        e.mg = (unsigned short)G.spvp;
     } else {
-        e.a = (short)(G.gray_cb + code * G.hp2);
+        e.a = (unsigned short)(G.gray_cb + code * G.hp2);
         e.m = 0;
-        e.g0 = (short)(code + G.gmg);
+        e.g0 = (unsigned short)(code + G.gmg);
         e.mg = 0;
     }
     return e;
