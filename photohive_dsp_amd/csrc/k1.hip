@@ -409,6 +409,9 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         // memory (L2-resident: its chunk was just loaded).  One pass of the fp64
         // path per <= kDq deferred pixels of the wave, where each lane redoing its
         // own ran it as often as the wave's busiest lane had pixels (~3 times).
+#if defined(PHD_K1_ABL_NODEFER)
+        emask = 0u;                  // timing experiment only (wrong sums): no deferred pass
+#endif
         {
             unsigned short* dq = reinterpret_cast<unsigned short*>(smem + V.dq) + (tid >> 6) * kDq;
             const int lane = lane_id();
@@ -461,7 +464,11 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
         merge = 5 * vote[16 * vpar] > (unsigned)(kT * kG);       // the next chunk's mode: > 1/5 of groups
         // fold the chunk's count words: one thread per cell sums its C copies;
         // the run's cell counts, the chunk's group counts, per-group sum kmax / n255
+#if defined(PHD_K1_ABL_NOFOLD)
+        for (int q = tid; q <= 0; q += kT) {   // timing experiment only (wrong counts): no chunk fold
+#else
         for (int q = tid; q <= ncell; q += kT) {
+#endif
             unsigned long long v = 0;
             for (int k = 0; k < C; k++) {
                 unsigned long long* wp = cnt + ((q << cshift) + k);
