@@ -78,52 +78,88 @@ __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
 
 // One thread's walk over E consecutive rows of a column: p per row in LDS
 // (lgb[r0 + j]), the column's bin runs in LDS (rl: start row << 16 | bin id,
-// ColRuns), idx = the run holding row r0.  Contiguous rows of one bin form a
-// run whose sum of log p is the log of its product: the frexp mantissas
-// multiply (>= 2^-E, no underflow), the exponents add, and one fp64 log
-// closes the run (pgm_normalize_fft's fp64 log, src/fft_processing.c:
+// ColRuns), sg = the thread's segment word (ColBins::seg: the run holding row
+// r0, bits 0-7, and the rows j > 0 where a run starts, bit 8 + j).  Contiguous
+// rows of one bin form a run whose sum of log p is the log of its product: the
+// frexp mantissas multiply (>= 2^-E, no underflow), the exponents add, and one
+// fp64 log closes the run (pgm_normalize_fft's fp64 log, src/fft_processing.c:
 // 196-199).  Each run adds bin_scale fixed point to its run's LDS slot (sl,
 // indexed like rl) with one LDS atomic (order-independent sums); the block
-// adds the column's slots to the image's bins afterwards.  A thread's first two runs are kept in
-// registers and logged after the walk: a wave then evaluates the fp64 log at
-// most twice (plus the rare third run of a thread), where logging inside the
-// unrolled walk ran it on almost every row (some lane of 64 changes bin there).
-template <int E>
+// adds the column's slots to the image's bins afterwards.
+//
+// Fast form (round 6), a wave whose lanes each meet at most two run starts
+// (~97 % of the waves of 4000x3000 / 72x40): branch-free, the starts f1 < f2
+// from the segment word, the product restarting at each and the first two
+// runs' products kept in registers; the wave then evaluates the fp64 log two
+// or three times.  Otherwise the general walk: the run list's entries in
+// registers, one branch per row (some lane of 64 changes bin on most rows).
+// Both multiply the same rows in the same order: identical bins.
+// HFULL: H % E == 0, so a thread with r0 < H has all E rows.
+template <int E, bool HFULL>
 __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0, int rend, const unsigned* rl,
-                                          int idx, unsigned long long* sl, double bscale,
+                                          unsigned sg, unsigned long long* sl, double bscale,
                                           const double2* __restrict__ lt) {
     auto flush = [&](int k, double m, int e) {
         const double acc = fmax((double)e * 0.69314718055994530942 + log_mant(m, lt), 0.0);
         atomicAdd(&sl[k], bin_fixed(acc, bscale));
     };
     if (r0 >= rend) return;
-    // the thread's first four entries in registers (one LDS latency), refilled
-    // one entry per run change; entries past the column's sentinel are never
-    // used (the sentinel's start is the height)
-    const unsigned q0 = rl[idx];
+    const int idx = (int)(sg & 255u);
+    const unsigned chm = sg >> 8;
+    if (__all(__popc(chm) <= 2)) {
+        const int f1 = __builtin_ctz(chm | 0x80000000u), f2 = __builtin_ctz((chm & (chm - 1)) | 0x80000000u);
+        double mp = 1.0, m0 = 1.0, m1 = 1.0;
+        int es = 0, e0 = 0, e1 = 0;
+#pragma unroll
+        for (int j = 0; j < E; j++) {
+            const int r = r0 + j;
+            if (HFULL || r < rend) {
+                const double pv = lgb[r];
+                if (j > 0) {
+                    const bool c1 = f1 == j, c2 = f2 == j;
+                    m0 = c1 ? mp : m0;
+                    e0 = c1 ? es : e0;
+                    m1 = c2 ? mp : m1;
+                    e1 = c2 ? es : e1;
+                    mp = (c1 || c2) ? 1.0 : mp;
+                    es = (c1 || c2) ? 0 : es;
+                }
+                int e;
+                mp *= frexp(pv, &e);
+                es += e;
+            }
+        }
+        const int n = __popc(chm);
+        flush(idx, n == 0 ? mp : m0, n == 0 ? es : e0);
+        if (n >= 1) flush(idx + 1, n == 1 ? mp : m1, n == 1 ? es : e1);
+        if (n == 2) flush(idx + 2, mp, es);
+        return;
+    }
+    // general walk: the thread's first four entries in registers (one LDS
+    // latency), refilled one entry per run change; entries past the column's
+    // sentinel are never used (the sentinel's start is the height).  A thread's
+    // first two runs are kept in registers and logged after the walk.
     unsigned q1 = rl[idx + 1], q2 = rl[min(idx + 2, kColRunsMax - 1)], q3 = rl[min(idx + 3, kColRunsMax - 1)];
     int qi = idx + 4;
     int cur = idx, nxt = (int)(q1 >> 16);                   // cur: the run's slot
-    (void)q0;
     int esum = 0, n = 0, b0 = 0, b1 = 0, e0 = 0, e1 = 0;
     // (round 6: the product in two interleaved chains, even / odd rows,
     // measured the same, 48.1-48.9 against 48.3-49.0 us: not the bound)
-    double mp[1] = {1.0};
+    double mp = 1.0;
     double m0 = 1.0, m1 = 1.0;
     auto close = [&]() {
-        const double mprod = mp[0];
         if (n == 0) {
-            b0 = cur; m0 = mprod; e0 = esum; n = 1;
+            b0 = cur; m0 = mp; e0 = esum; n = 1;
         } else if (n == 1) {
-            b1 = cur; m1 = mprod; e1 = esum; n = 2;
+            b1 = cur; m1 = mp; e1 = esum; n = 2;
         } else {
-            flush(cur, mprod, esum);
+            flush(cur, mp, esum);
         }
     };
 #pragma unroll
     for (int j = 0; j < E; j++) {
         const int r = r0 + j;
-        if (r < rend) {
+        if (HFULL || r < rend) {
             const double pv = lgb[r];
             if (r >= nxt) {                       // the next run starts here (runs are never empty)
                 close();
@@ -132,11 +168,11 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
                 q2 = q3;
                 q3 = rl[min(qi++, kColRunsMax - 1)];
                 nxt = (int)(q1 >> 16);
-                mp[0] = 1.0;
+                mp = 1.0;
                 esum = 0;
             }
             int e;
-            mp[0] *= frexp(pv, &e);
+            mp *= frexp(pv, &e);
             esum += e;
         }
     }
@@ -391,7 +427,7 @@ __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70)
 template <int H, int T, bool FULL, int... Rs>
 __global__ __launch_bounds__(T, (ColK<H, T, FULL, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
                                                      const unsigned* __restrict__ runs,
-                                                     const uint8_t* __restrict__ segidx, int rstride,
+                                                     const unsigned* __restrict__ segidx, int rstride,
                                                      unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums0, int width,
@@ -479,10 +515,10 @@ __global__ __launch_bounds__(T, (ColK<H, T, FULL, Rs...>::MINW)) void k_cols_ct(
         const int col = 2 * (2 * u + (quad >> 1)) + half;
         const bool live = col < wf;                       // the phantom column of an odd wf idles
         // the column's bin runs (image-independent, ~0.3 KB per column; ColRuns)
-        // and the run holding this thread's first row tid * E: loaded now, stored
+        // and this thread's segment word (walk_runs): loaded now, the list stored
         // to LDS after the FFT (a phantom column reads column 0's: its p are 1)
         unsigned rreg[K::RPT];
-        int sidx;
+        unsigned sidx;
         {
             const int rc = live ? col : 0;
             const unsigned* rsrc = runs + (size_t)rc * rstride;
@@ -544,7 +580,7 @@ __global__ __launch_bounds__(T, (ColK<H, T, FULL, Rs...>::MINW)) void k_cols_ct(
         if (u + 1 < un && !pf_late) dma(u + 1, K::PF ? 0 : 1);
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
-        if (!(ablate & 2)) walk_runs<K::E>(lgb, tid * K::E, H, rl, sidx, sl, bscale, lt);
+        if (!(ablate & 2)) walk_runs<K::E, H % K::E == 0>(lgb, tid * K::E, H, rl, sidx, sl, bscale, lt);
         __syncthreads();
         if (!K::PF && u + 1 < un && !pf_late) dma(u + 1, 2);   // p is read: the lower half too
         // the column's run sums into the image's bins (a bin met by two runs of
