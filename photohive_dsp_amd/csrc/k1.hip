@@ -145,6 +145,31 @@ struct Mom {
 // thread that land in the same cell are summed in registers and added to the
 // LDS with one set of atomics when the cell changes (flat image regions put
 // most of a wave's lanes on one address, where LDS atomics serialise).
+// Sums over the wave of a small per-lane count v < 2^B by bit slices: one
+// ballot per bit, counted with s_bcnt1 (and mbcnt for the lanes below this
+// one), instead of six cross-lane shuffles, each an LDS round trip of ~100+
+// cycles on the chunk's critical path (round 6).
+template <int B>
+__device__ __forceinline__ unsigned wave_sum_bits(unsigned v) {
+    unsigned t = 0;
+#pragma unroll
+    for (int b = 0; b < B; b++) t += (unsigned)__popcll(__ballot((v >> b) & 1u)) << b;
+    return t;
+}
+// the exclusive prefix over the lanes below this one; the wave's total in tot
+template <int B>
+__device__ __forceinline__ unsigned wave_prefix_bits(unsigned v, unsigned& tot) {
+    unsigned pre = 0, t = 0;
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+        const unsigned long long m = __ballot((v >> b) & 1u);
+        pre += __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)) << b;
+        t += (unsigned)__popcll(m) << b;
+    }
+    tot = t;
+    return pre;
+}
+
 struct CellRun {
     int cell;            // -1: empty
     int grp;
@@ -383,8 +408,9 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             };
             if (merge) loop(std::true_type{});
             else loop(std::false_type{});
-            const unsigned long long nw = wave_sum((unsigned long long)nsame);
-            if (lane_id() == 0) atomicAdd(&vote[16 * vpar], (unsigned)nw);
+            static_assert(kG < 16, "nsame <= kG: four bit slices");
+            const unsigned nw = wave_sum_bits<4>(nsame);
+            if (lane_id() == 0) atomicAdd(&vote[16 * vpar], nw);
         }
         const bool last_chunk = base + kChunk >= npix;            // block-uniform
         if (last_chunk && tid == 0) {
@@ -416,16 +442,10 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             unsigned short* dq = reinterpret_cast<unsigned short*>(smem + V.dq) + (tid >> 6) * kDq;
             const int lane = lane_id();
             while (true) {                                        // wave-uniform
-                const int cnt = __popc(emask);
-                int incl = cnt;                                   // inclusive scan over the wave
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int y = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += y;
-                }
-                const int total = __shfl(incl, 63, 64);
+                unsigned utot;                                    // cnt <= 32: six bit slices
+                int off = (int)wave_prefix_bits<6>((unsigned)__popc(emask), utot);
+                const int total = (int)utot;
                 if (total == 0) break;
-                int off = incl - cnt;
                 while (emask && off < kDq) {                      // what fits this round
                     const int bt = __ffs(emask) - 1;
                     emask &= emask - 1;
