@@ -245,18 +245,25 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     if (live) fetch(im, pr);
     __syncthreads();
     unsigned cs[3] = {0u, 0u, 0u};    // this thread's channel sums (u32: a few row pairs of bytes)
+#if defined(PHD_ROW_NOSWZ)
+    const int rot = 0;                // A/B build: no write swizzle
+#else
     const int rot = (tid >> 1) & 3;   // b128 write swizzle: 8 lanes of a group hit 8 distinct 16-B slots
+#endif
     // one row pair.  The loop head is reached with the same memory operations in
     // flight on every path (the prefetch, then the stores: a step's or, before
     // the first step, as many dummy stores to a per-block slot), so the wait for
     // the prefetched pixels counts the stores instead of draining them.
-    constexpr int WF_ = W / 2 + 1, KP_ = (WF_ + 1) / 2, NSO_ = (4 * KP_ + T - 1) / T;
+    constexpr int WF_ = W / 2 + 1, NK_ = 2 * ((WF_ + 1) / 2), NSK_ = (NK_ + T - 1) / T;
     {
         // a scratch run just past the tiles (inter_elems: 1024 elements of slack)
-        double2* slot = inter + (size_t)P * ct_row_stride(W) + (blockIdx.x & 63) * NSO_;
+        double2* slot = inter + (size_t)P * ct_row_stride(W) + (blockIdx.x & 63) * 2 * NSK_;
 #pragma unroll
-        for (int j = 0; j < NSO_; j++)
-            if ((4 * KP_) % T == 0 || tid + j * T < 4 * KP_) slot[j] = make_double2(0.0, 0.0);
+        for (int j = 0; j < NSK_; j++)
+            if (NK_ % T == 0 || tid + j * T < NK_) {
+                slot[2 * j] = make_double2(0.0, 0.0);
+                slot[2 * j + 1] = make_double2(0.0, 0.0);
+            }
     }
     auto step = [&]() __attribute__((always_inline)) {
         const int y0 = 2 * pr;
@@ -297,32 +304,33 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
         if (!(ablate & 4)) fetch(next ? imn : im, next ? prn : pr);
         __syncthreads();
         if (!(ablate & 1)) fft_lds<W, T, 1, Rs...>(buf, tw, tid);
-        constexpr int WF = W / 2 + 1, KP = (WF + 1) / 2;
+        constexpr int WF = W / 2 + 1, NK = 2 * ((WF + 1) / 2);
         // the pair's tile row, contiguous and 128-byte aligned (ct_row_stride):
-        // thread i -> (column pair i/4, column k = 2(i/4) + (i/2)%2, row y0 +
-        // i%2); the phantom column WF (odd WF) is 0 (a fixed, unrolled count per
-        // thread, branch-free: the next step's wait for its prefetched pixels can
-        // then count these stores exactly)
+        // thread i -> column k = i, both rows: elements 2k (row y0) and 2k + 1
+        // (row y0 + 1) of the row, i.e. (column pair k/2, column k, rows y0 and
+        // y0 + 1), 32 contiguous bytes; the phantom column WF (odd WF) is 0.
+        // (Round 6: one thread per column and both rows, where one per element
+        // read each Z twice and selected its operands by row per lane.)  A
+        // fixed, unrolled count per thread, branch-free: the next step's wait for
+        // its prefetched pixels can then count these stores exactly.
         // (ablation bit 8, timing builds: every block stores to one of 8 fixed
         // tile rows, so the stores stay L2-resident -- the row-pass FETCH study)
         double2* orow = inter + ((ablate & 8) ? (size_t)(blockIdx.x & 7) * ct_row_stride(W)
                                               : im * istride + (size_t)pr * ct_row_stride(W));
-        constexpr int NSO = (4 * KP + T - 1) / T;
+        constexpr int NSK = (NK + T - 1) / T;
 #pragma unroll
-        for (int j = 0; j < NSO; j++) {
-            const int i = tid + j * T;
-            if ((4 * KP) % T == 0 || i < 4 * KP) {
+        for (int j = 0; j < NSK; j++) {
+            const int k = tid + j * T;
+            if (NK % T == 0 || k < NK) {
                 if (ablate & 2) continue;
-                const int k = 2 * (i >> 2) + ((i >> 1) & 1);
-                const bool second = i & 1;
                 const int kk = k < WF ? k : 0;
                 const double2 zk = buf[kk], zm = buf[kk == 0 ? 0 : W - kk];
                 // first row: (Z[k] + conj Z[W-k]) / 2; second: (Z[k] - conj Z[W-k]) / 2i
-                const double ax = second ? zk.y : zk.x, bx = second ? zm.y : zm.x;
-                const double ay = second ? zk.x : zk.y, by = second ? zm.x : zm.y;
-                const bool keep = k < WF && (two || !second);
-                const double re = 0.5 * (ax + bx), im = (second ? -0.5 : 0.5) * (ay - by);
-                orow[i] = make_double2(keep ? re : 0.0, keep ? im : 0.0);
+                const bool live = k < WF, live2 = live && two;
+                const double ar = 0.5 * (zk.x + zm.x), ai = 0.5 * (zk.y - zm.y);
+                const double br = 0.5 * (zk.y + zm.y), bi = -0.5 * (zk.x - zm.x);
+                orow[2 * k] = make_double2(live ? ar : 0.0, live ? ai : 0.0);
+                orow[2 * k + 1] = make_double2(live2 ? br : 0.0, live2 ? bi : 0.0);
             }
         }
         __syncthreads();
