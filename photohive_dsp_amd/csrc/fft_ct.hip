@@ -76,6 +76,21 @@ __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
     return (x >> (8 * (b & 3))) & 255;
 }
 
+// The 4 pixels of a 12-byte group rotated by r (0-3) pixels, i.e. its bytes
+// by 3 r = 4 q + sh: pixel e of the result is pixel (e + r) & 3 of w (word i
+// of the result: bytes sh.. of word q + i and the low bytes of word q + i + 1)
+[[maybe_unused]] __device__ __forceinline__ u32x3a rot_px(const u32x3a& w, int r) {
+    const int b = 3 * r, q = b >> 2, sh = b & 3;
+    const unsigned l0 = q == 0 ? w.x : (q == 1 ? w.y : w.z);
+    const unsigned l1 = q == 0 ? w.y : (q == 1 ? w.z : w.x);
+    const unsigned l2 = q == 0 ? w.z : (q == 1 ? w.x : w.y);
+    u32x3a o;
+    o.x = __builtin_amdgcn_alignbyte(l1, l0, (unsigned)sh);
+    o.y = __builtin_amdgcn_alignbyte(l2, l1, (unsigned)sh);
+    o.z = __builtin_amdgcn_alignbyte(l0, l2, (unsigned)sh);
+    return o;
+}
+
 // One thread's walk over E consecutive rows of a column: p per row in LDS
 // (lgb[r0 + j]), the column's bin runs in LDS (rl: start row << 16 | bin id,
 // ColRuns), sg = the thread's segment word (ColBins::seg: the run holding row
@@ -254,16 +269,13 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     // flight on every path (the prefetch, then the stores: a step's or, before
     // the first step, as many dummy stores to a per-block slot), so the wait for
     // the prefetched pixels counts the stores instead of draining them.
-    constexpr int WF_ = W / 2 + 1, NK_ = 2 * ((WF_ + 1) / 2), NSK_ = (NK_ + T - 1) / T;
+    constexpr int WF_ = W / 2 + 1, KP_ = (WF_ + 1) / 2, NSO_ = (4 * KP_ + T - 1) / T;
     {
         // a scratch run just past the tiles (inter_elems: 1024 elements of slack)
-        double2* slot = inter + (size_t)P * ct_row_stride(W) + (blockIdx.x & 63) * 2 * NSK_;
+        double2* slot = inter + (size_t)P * ct_row_stride(W) + (blockIdx.x & 63) * NSO_;
 #pragma unroll
-        for (int j = 0; j < NSK_; j++)
-            if (NK_ % T == 0 || tid + j * T < NK_) {
-                slot[2 * j] = make_double2(0.0, 0.0);
-                slot[2 * j + 1] = make_double2(0.0, 0.0);
-            }
+        for (int j = 0; j < NSO_; j++)
+            if ((4 * KP_) % T == 0 || tid + j * T < 4 * KP_) slot[j] = make_double2(0.0, 0.0);
     }
     auto step = [&]() __attribute__((always_inline)) {
         const int y0 = 2 * pr;
@@ -273,28 +285,40 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
             const int g = tid + j * T;
             if (K::G4 % T == 0 || g < K::G4) {
                 double2 z[4];
+#if defined(PHD_ROW_ROTW)
+                // the swizzle on the bytes (pixel e of w0 / w1 is pixel (e + rot) & 3)
+                const u32x3a w0 = rot_px(rg[j][0], rot), w1 = rot_px(rg[j][1], rot);
+#else
+                const u32x3a& w0 = rg[j][0];
+                const u32x3a& w1 = rg[j][1];
+#endif
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     // rgb2pgm (src/image_processing.c:509) with k/255 folded into the
                     // weights (within 2 ulp); remove_dc_bias is the column pass's
-                    const double p0 = kWr * byte_of(rg[j][0], 3 * e) + kWg * byte_of(rg[j][0], 3 * e + 1) +
-                                      kWb * byte_of(rg[j][0], 3 * e + 2);
-                    const double p1 = kWr * byte_of(rg[j][1], 3 * e) + kWg * byte_of(rg[j][1], 3 * e + 1) +
-                                      kWb * byte_of(rg[j][1], 3 * e + 2);
+                    const double p0 = kWr * byte_of(w0, 3 * e) + kWg * byte_of(w0, 3 * e + 1) +
+                                      kWb * byte_of(w0, 3 * e + 2);
+                    const double p1 = kWr * byte_of(w1, 3 * e) + kWg * byte_of(w1, 3 * e + 1) +
+                                      kWb * byte_of(w1, 3 * e + 2);
                     z[e] = make_double2(p0, two ? p1 : 0.0);
                     // rsum (the blur-only path, which runs no K1): the channel sums
                     // of the column pass's DC bias, exact integers
                     if (rsum) {                                   // uniform
-                        cs[0] += byte_of(rg[j][0], 3 * e) + (two ? byte_of(rg[j][1], 3 * e) : 0);
-                        cs[1] += byte_of(rg[j][0], 3 * e + 1) + (two ? byte_of(rg[j][1], 3 * e + 1) : 0);
-                        cs[2] += byte_of(rg[j][0], 3 * e + 2) + (two ? byte_of(rg[j][1], 3 * e + 2) : 0);
+                        cs[0] += byte_of(w0, 3 * e) + (two ? byte_of(w1, 3 * e) : 0);
+                        cs[1] += byte_of(w0, 3 * e + 1) + (two ? byte_of(w1, 3 * e + 1) : 0);
+                        cs[2] += byte_of(w0, 3 * e + 2) + (two ? byte_of(w1, 3 * e + 2) : 0);
                     }
                 }
+#if defined(PHD_ROW_ROTW)
+#pragma unroll
+                for (int e = 0; e < 4; e++) buf[4 * g + ((e + rot) & 3)] = z[e];
+#else
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     const int ee = (e + rot) & 3;
                     buf[4 * g + ee] = sel4(ee, z[0], z[1], z[2], z[3]);
                 }
+#endif
             }
         }
         // unconditional (past the last pair it re-reads this one): every path into
@@ -304,33 +328,36 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
         if (!(ablate & 4)) fetch(next ? imn : im, next ? prn : pr);
         __syncthreads();
         if (!(ablate & 1)) fft_lds<W, T, 1, Rs...>(buf, tw, tid);
-        constexpr int WF = W / 2 + 1, NK = 2 * ((WF + 1) / 2);
+        constexpr int WF = W / 2 + 1, KP = (WF + 1) / 2;
         // the pair's tile row, contiguous and 128-byte aligned (ct_row_stride):
-        // thread i -> column k = i, both rows: elements 2k (row y0) and 2k + 1
-        // (row y0 + 1) of the row, i.e. (column pair k/2, column k, rows y0 and
-        // y0 + 1), 32 contiguous bytes; the phantom column WF (odd WF) is 0.
-        // (Round 6: one thread per column and both rows, where one per element
-        // read each Z twice and selected its operands by row per lane.)  A
-        // fixed, unrolled count per thread, branch-free: the next step's wait for
-        // its prefetched pixels can then count these stores exactly.
+        // thread i -> (column pair i/4, column k = 2(i/4) + (i/2)%2, row y0 +
+        // i%2); the phantom column WF (odd WF) is 0 (a fixed, unrolled count per
+        // thread, branch-free: the next step's wait for its prefetched pixels can
+        // then count these stores exactly)
+        // (round 6: one thread per column writing both rows' 32 contiguous bytes
+        // -- half the LDS reads, no per-lane operand selects -- measured slower,
+        // 44.6-45.8 against 42.3-42.7 us: its stores cover each 1 KB span in two
+        // half-density instructions)
         // (ablation bit 8, timing builds: every block stores to one of 8 fixed
         // tile rows, so the stores stay L2-resident -- the row-pass FETCH study)
         double2* orow = inter + ((ablate & 8) ? (size_t)(blockIdx.x & 7) * ct_row_stride(W)
                                               : im * istride + (size_t)pr * ct_row_stride(W));
-        constexpr int NSK = (NK + T - 1) / T;
+        constexpr int NSO = (4 * KP + T - 1) / T;
 #pragma unroll
-        for (int j = 0; j < NSK; j++) {
-            const int k = tid + j * T;
-            if (NK % T == 0 || k < NK) {
+        for (int j = 0; j < NSO; j++) {
+            const int i = tid + j * T;
+            if ((4 * KP) % T == 0 || i < 4 * KP) {
                 if (ablate & 2) continue;
+                const int k = 2 * (i >> 2) + ((i >> 1) & 1);
+                const bool second = i & 1;
                 const int kk = k < WF ? k : 0;
                 const double2 zk = buf[kk], zm = buf[kk == 0 ? 0 : W - kk];
                 // first row: (Z[k] + conj Z[W-k]) / 2; second: (Z[k] - conj Z[W-k]) / 2i
-                const bool live = k < WF, live2 = live && two;
-                const double ar = 0.5 * (zk.x + zm.x), ai = 0.5 * (zk.y - zm.y);
-                const double br = 0.5 * (zk.y + zm.y), bi = -0.5 * (zk.x - zm.x);
-                orow[2 * k] = make_double2(live ? ar : 0.0, live ? ai : 0.0);
-                orow[2 * k + 1] = make_double2(live2 ? br : 0.0, live2 ? bi : 0.0);
+                const double ax = second ? zk.y : zk.x, bx = second ? zm.y : zm.x;
+                const double ay = second ? zk.x : zk.y, by = second ? zm.x : zm.y;
+                const bool keep = k < WF && (two || !second);
+                const double re = 0.5 * (ax + bx), im = (second ? -0.5 : 0.5) * (ay - by);
+                orow[i] = make_double2(keep ? re : 0.0, keep ? im : 0.0);
             }
         }
         __syncthreads();

@@ -92,6 +92,15 @@ K1_HD K1Inv k1_inv_p(int p, int km1) {      // p = kd1 km1 (the kernel forms it 
 }
 K1_HD K1Inv k1_inv_pair(int kd1, int km1) { return k1_inv_p(k1_mul(kd1, km1), km1); }
 
+// 1 / x in fp32: v_rcp_f32 on the device (<= 1 ulp), correctly rounded on the host
+K1_HD float k1_rcpf(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+
 // q - floor(q) for 0 <= q < 2^23 (exact in fp32)
 K1_HD float k1_fract(float q, int c) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -313,7 +322,9 @@ K1_HD K1Px k1_exact(int kr, int kg, int kb, int code, double Lh, const double* k
     const int t1 = isg ? kb - kr : kr - kg;
     const int X = isr ? kg - kb + (kg < kb ? 6 * kd : 0) : (kd << (isg ? 1 : 2)) + t1;
     const int n2 = 120 * X;
-    const int c = k1_halfbin(n2, 1.0f / (float)kd1, G);             // as k1_pixel: exact
+    // (round 6: v_rcp_f32 on the device, the <= 1 ulp k1_halfbin allows, where
+    // 1.0f / kd1 was a correctly rounded division of ~12 instructions)
+    const int c = k1_halfbin(n2, k1_rcpf((float)kd1), G);           // as k1_pixel: exact
     const double B = (double)c * (double)G.lh * 0.5;
     const int ch = c - G.hp;
     int below;
@@ -336,7 +347,10 @@ K1_HD K1Px k1_exact(int kr, int kg, int kb, int code, double Lh, const double* k
     p.lo = 1u + ((unsigned)((kmx + 1) >> 8) << 16);
     p.hi = (unsigned)kmx;
     p.h = h;
-    p.s = kmx == 0 ? 0.0 : (kmn == 0 ? 0.999999 : (double)kd * (1.0 / (double)kmx));
+    // s as the fast path's (kd^2 / (kd1 km1) through k1_inv_pair, ~2^-45
+    // relative; round 6, where kd * (1.0 / kmx) took an fp64 division)
+    const int km1 = kmx > 1 ? kmx : 1;
+    p.s = kmn == 0 && kmx != 0 ? 0.999999 : (double)k1_mul(kd, kd) * k1_inv_pair(kd1, km1).inv;
     return p;
 }
 
