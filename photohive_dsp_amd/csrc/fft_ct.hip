@@ -56,10 +56,6 @@ namespace {
 
 using namespace fe;
 
-__device__ __forceinline__ double2 sel4(int e, double2 a, double2 b, double2 c, double2 d) {
-    return e == 0 ? a : (e == 1 ? b : (e == 2 ? c : d));
-}
-
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // a native 128-bit register tuple
 
 constexpr double kWr = 0.299 / 255.0, kWg = 0.587 / 255.0, kWb = 0.114 / 255.0;
@@ -79,7 +75,7 @@ __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
 // The 4 pixels of a 12-byte group rotated by r (0-3) pixels, i.e. its bytes
 // by 3 r = 4 q + sh: pixel e of the result is pixel (e + r) & 3 of w (word i
 // of the result: bytes sh.. of word q + i and the low bytes of word q + i + 1)
-[[maybe_unused]] __device__ __forceinline__ u32x3a rot_px(const u32x3a& w, int r) {
+__device__ __forceinline__ u32x3a rot_px(const u32x3a& w, int r) {
     const int b = 3 * r, q = b >> 2, sh = b & 3;
     const unsigned l0 = q == 0 ? w.x : (q == 1 ? w.y : w.z);
     const unsigned l1 = q == 0 ? w.y : (q == 1 ? w.z : w.x);
@@ -260,11 +256,9 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
     if (live) fetch(im, pr);
     __syncthreads();
     unsigned cs[3] = {0u, 0u, 0u};    // this thread's channel sums (u32: a few row pairs of bytes)
-#if defined(PHD_ROW_NOSWZ)
-    const int rot = 0;                // A/B build: no write swizzle
-#else
-    const int rot = (tid >> 1) & 3;   // b128 write swizzle: 8 lanes of a group hit 8 distinct 16-B slots
-#endif
+    // b128 write swizzle: 8 lanes of a group hit 8 distinct 16-B slots (the
+    // group's pixels rotated by rot in its bytes, rot_px)
+    const int rot = (tid >> 1) & 3;
     // one row pair.  The loop head is reached with the same memory operations in
     // flight on every path (the prefetch, then the stores: a step's or, before
     // the first step, as many dummy stores to a per-block slot), so the wait for
@@ -285,13 +279,12 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
             const int g = tid + j * T;
             if (K::G4 % T == 0 || g < K::G4) {
                 double2 z[4];
-#if defined(PHD_ROW_ROTW)
-                // the swizzle on the bytes (pixel e of w0 / w1 is pixel (e + rot) & 3)
+                // the swizzle on the bytes: pixel e of w0 / w1 is pixel (e + rot) & 3,
+                // stored to its own slot.  (Round 6: 41.1-41.2 us against 42.2-42.7
+                // for selecting the rotated values as doubles, 48 v_cndmask per
+                // group, and 42.0-42.7 without a swizzle; profiles/r06/
+                // row_swizzle_ab.log)
                 const u32x3a w0 = rot_px(rg[j][0], rot), w1 = rot_px(rg[j][1], rot);
-#else
-                const u32x3a& w0 = rg[j][0];
-                const u32x3a& w1 = rg[j][1];
-#endif
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
                     // rgb2pgm (src/image_processing.c:509) with k/255 folded into the
@@ -309,16 +302,8 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
                         cs[2] += byte_of(w0, 3 * e + 2) + (two ? byte_of(w1, 3 * e + 2) : 0);
                     }
                 }
-#if defined(PHD_ROW_ROTW)
 #pragma unroll
                 for (int e = 0; e < 4; e++) buf[4 * g + ((e + rot) & 3)] = z[e];
-#else
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int ee = (e + rot) & 3;
-                    buf[4 * g + ee] = sel4(ee, z[0], z[1], z[2], z[3]);
-                }
-#endif
             }
         }
         // unconditional (past the last pair it re-reads this one): every path into
