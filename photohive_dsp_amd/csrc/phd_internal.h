@@ -188,6 +188,11 @@ hipError_t launch_hsv_stats_batch(const uint8_t* const* d_imgs, int n, int heigh
 // a batch of 4-byte-aligned images: stats.hip (out0.sums, out0.s_part).
 hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width, const PaletteDev& out0,
                                   long a_stride, int nchunks, hipStream_t st);
+// The statistics batch's per-image finish (stats.hip): from n A records
+// (a_stride apart: six u64 moments, chunk s partials at s_off, 256 sums of d
+// per max value at kd_off) to out[8 i ..]: the moments, then sum(s) / npix.
+hipError_t launch_stats_finish(const uint8_t* rec, int n, long a_stride, long s_off, long kd_off, int nchunks,
+                               long npix, unsigned long long* out, hipStream_t st);
 // The fused K1 of k1.hip (table classification, packed counts): cshift of its
 // lane-private copies, or -1 when this grid does not fit it (palette.hip's
 // fused K1 then runs).

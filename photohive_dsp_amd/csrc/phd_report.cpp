@@ -1210,7 +1210,9 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
     const size_t a_kd = al(6 * sizeof(unsigned long long)) + al(sizeof(double) * nchunks);
     const size_t a_stride = a_kd + al(256 * sizeof(unsigned long long));
     const size_t rec = (size_t)n_images * a_stride, ptrs = al(sizeof(void*) * (size_t)n_images);
-    if (!ensure_device(&c->d_ws, &c->ws_bytes, rec + ptrs) || !ensure_pinned(c, rec + ptrs)) return -1;
+    const size_t fin = (size_t)n_images * 8 * sizeof(unsigned long long);   // k_stats_finish's records
+    if (!ensure_device(&c->d_ws, &c->ws_bytes, rec + ptrs + fin) || !ensure_pinned(c, rec + ptrs + fin))
+        return -1;
     uint8_t* dw = (uint8_t*)c->d_ws;
     uint8_t* hp = (uint8_t*)c->h_pin;
     const uint8_t** hptr = (const uint8_t**)(hp + rec);
@@ -1236,22 +1238,20 @@ extern "C" int phd_hsv_stats_batch_device(const uint8_t* d_rgb, int n_images, in
                                     all_aligned(hptr, n_images), st)) != hipSuccess)
         return fail(e, "launch");
     c->prof.end(ps, st);
-    if ((e = hipMemcpyAsync(hp, dw, rec, hipMemcpyDeviceToHost, st)) != hipSuccess) return fail(e, "readback");
+    // sum(s) = the chunk s partials (the partial final group and -(1 - 0.999999)
+    // per min == 0 < max pixel) + sum_m (sum of d at max m) / m, finished on the
+    // device per image (k_stats_finish): 64 bytes per image come back
+    unsigned long long* dfin = (unsigned long long*)(dw + rec + ptrs);
+    if ((e = launch_stats_finish(dw, n_images, (long)a_stride, (long)al(6 * sizeof(unsigned long long)),
+                                 (long)a_kd, nchunks, npix, dfin, st)) != hipSuccess)
+        return fail(e, "finish launch");
+    if ((e = hipMemcpyAsync(hp, dfin, fin, hipMemcpyDeviceToHost, st)) != hipSuccess) return fail(e, "readback");
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return fail(e, "sync");
     c->prof.collect();
+    const unsigned long long* hf = (const unsigned long long*)hp;
     for (int i = 0; i < n_images; i++) {
-        const uint8_t* a = hp + (size_t)i * a_stride;
-        stats[i] = stats_from_sums((const unsigned long long*)a, npix);
-        const double* sp = (const double*)(a + al(6 * sizeof(unsigned long long)));
-        // sum(s) = per-run s partials (the fp32 modes; in the exact mode only the
-        // partial final group and -(1 - 0.999999) per min == 0 < max pixel) +
-        // sum_m (sum of d at max m) / m (the exact mode; zero otherwise)
-        const unsigned long long* kd = (const unsigned long long*)(a + a_kd);
-        double sacc = 0.0;
-        for (int k = 0; k < nchunks; k++) sacc += sp[k];
-        for (int m = 1; m < 256; m++)
-            if (kd[m]) sacc += (double)kd[m] / (double)m;
-        avg_saturation[i] = sacc / (double)npix;
+        stats[i] = stats_from_sums(hf + 8 * (size_t)i, npix);
+        avg_saturation[i] = __builtin_bit_cast(double, hf[8 * (size_t)i + 6]);
     }
     return 0;
 }

@@ -210,7 +210,37 @@ __global__ __launch_bounds__(kStThreads, 8) void k_rgb_stats(const uint8_t* cons
     }
 }
 
+// The batch's per-image finish on the device (round 6; the host loop over
+// each image's chunk partials and 255 sums of d per max value was ~0.2 ms of
+// host time per 512-image call): one wave per image sums sum(s) = its chunk
+// partials + sum_m (sum of d at max m) / m in a fixed order (strided lanes,
+// then the xor butterfly: deterministic), and copies the six moments.  out:
+// 8 u64 per image, the moments then the bits of sum(s) / npix.
+__global__ __launch_bounds__(64) void k_stats_finish(const uint8_t* __restrict__ rec, long a_stride, long s_off,
+                                                     long kd_off, int nchunks, long npix,
+                                                     unsigned long long* __restrict__ out) {
+    const int i = blockIdx.x, lane = threadIdx.x;
+    const uint8_t* a = rec + (size_t)i * a_stride;
+    const double* sp = reinterpret_cast<const double*>(a + s_off);
+    const unsigned long long* kd = reinterpret_cast<const unsigned long long*>(a + kd_off);
+    double s = 0.0;
+    for (int k = lane; k < nchunks; k += 64) s += sp[k];
+    for (int m = lane; m < 256; m += 64)
+        if (m > 0 && kd[m]) s += (double)kd[m] / (double)m;
+    s = wave_sum(s);
+    unsigned long long* o = out + (size_t)i * 8;
+    if (lane < 6) o[lane] = reinterpret_cast<const unsigned long long*>(a)[lane];
+    if (lane == 0) o[6] = __builtin_bit_cast(unsigned long long, s / (double)npix);
+}
+
 }  // namespace
+
+hipError_t launch_stats_finish(const uint8_t* rec, int n, long a_stride, long s_off, long kd_off, int nchunks,
+                               long npix, unsigned long long* out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    phd_launch(k_stats_finish, dim3(n), dim3(64), 0, st, rec, a_stride, s_off, kd_off, nchunks, npix, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_rgb_stats_batch(const uint8_t* const* d_imgs, int n, int height, int width, const PaletteDev& out0,
                                   long a_stride, int nchunks, hipStream_t st) {
