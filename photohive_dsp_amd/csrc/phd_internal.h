@@ -301,7 +301,7 @@ int fft_cols_blocks(int height, int wf, int nbins, const FftPlan& plan, size_t* 
     X(480, 128, 5, 6, 16)        \
     X(512, 64, 8, 8, 8)
 // (the 3000-row plan's threads and radices are overridable for A/B builds:
-// make variant VFLAGS='-DPHD_C3000_T=320 "-DPHD_C3000_R=20, 15, 10"')
+// make variant VFLAGS="-DPHD_C3000_T=320 -DPHD_C3000_R=20,15,10")
 #ifndef PHD_C3000_T
 #define PHD_C3000_T 256
 #endif
