@@ -72,6 +72,15 @@ __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
     return (x >> (8 * (b & 3))) & 255;
 }
 
+// x of the lane next to this one in its pair (lanes 2m, 2m + 1), by DPP
+// (quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ double dpp_pair_swap(double x) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, 0xB1, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), 0xB1, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
 // The 4 pixels of a 12-byte group rotated by r (0-3) pixels, i.e. its bytes
 // by 3 r = 4 q + sh: pixel e of the result is pixel (e + r) & 3 of w (word i
 // of the result: bytes sh.. of word q + i and the low bytes of word q + i + 1)
@@ -336,13 +345,21 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
                 const int k = 2 * (i >> 2) + ((i >> 1) & 1);
                 const bool second = i & 1;
                 const int kk = k < WF ? k : 0;
-                const double2 zk = buf[kk], zm = buf[kk == 0 ? 0 : W - kk];
-                // first row: (Z[k] + conj Z[W-k]) / 2; second: (Z[k] - conj Z[W-k]) / 2i
-                const double ax = second ? zk.y : zk.x, bx = second ? zm.y : zm.x;
-                const double ay = second ? zk.x : zk.y, by = second ? zm.x : zm.y;
-                const bool keep = k < WF && (two || !second);
-                const double re = 0.5 * (ax + bx), im = (second ? -0.5 : 0.5) * (ay - by);
-                orow[i] = make_double2(keep ? re : 0.0, keep ? im : 0.0);
+                // first row: (Z[k] + conj Z[W-k]) / 2; second: (Z[k] - conj Z[W-k]) / 2i.
+                // The lanes i, i + 1 (one column k) split the reads (round 6): the
+                // even lane reads Z[k] as (A, B) = (x, y), the odd lane Z[W-k] with
+                // its halves swapped, (A, B) = (y, x), and each takes its
+                // partner's (A', B') by DPP.  Both rows are then re = (A + B') / 2,
+                // im = (B - A') / 2 (first: Z[k].x + Z[W-k].x, Z[k].y - Z[W-k].y;
+                // second: Z[W-k].y + Z[k].y, Z[W-k].x - Z[k].x): one b64 read pair
+                // per element and no operand selects, where each lane read both Z
+                // and selected its operands by row.
+                const int e = second ? (kk == 0 ? 0 : W - kk) : kk;
+                const double* zp = reinterpret_cast<const double*>(buf + e);
+                const double A = zp[second ? 1 : 0], B = zp[second ? 0 : 1];
+                const double Ap = dpp_pair_swap(A), Bp = dpp_pair_swap(B);
+                const double f = (k < WF && (two || !second)) ? 0.5 : 0.0;   // 0: the phantom column / row
+                orow[i] = make_double2(f * (A + Bp), f * (B - Ap));
             }
         }
         __syncthreads();
