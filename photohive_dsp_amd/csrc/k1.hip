@@ -141,10 +141,6 @@ struct Mom {
     unsigned sr, sg, sb, qr, qg, qb;
 };
 
-// A thread's run of pixels in one hue cell (MERGE): consecutive pixels of a
-// thread that land in the same cell are summed in registers and added to the
-// LDS with one set of atomics when the cell changes (flat image regions put
-// most of a wave's lanes on one address, where LDS atomics serialise).
 // Sums over the wave of a small per-lane count v < 2^B by bit slices: one
 // ballot per bit, counted with s_bcnt1 (and mbcnt for the lanes below this
 // one), instead of six cross-lane shuffles, each an LDS round trip of ~100+
@@ -170,6 +166,10 @@ __device__ __forceinline__ unsigned wave_prefix_bits(unsigned v, unsigned& tot) 
     return pre;
 }
 
+// A thread's run of pixels in one hue cell (MERGE): consecutive pixels of a
+// thread that land in the same cell are summed in registers and added to the
+// LDS with one set of atomics when the cell changes (flat image regions put
+// most of a wave's lanes on one address, where LDS atomics serialise).
 struct CellRun {
     int cell;            // -1: empty
     int grp;
