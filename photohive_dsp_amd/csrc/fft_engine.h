@@ -279,6 +279,10 @@ __device__ __forceinline__ void fft_lds(double2* buf, const double2* tw, int tid
     if constexpr (sizeof...(Rest) > 0) fft_lds<N, T, NS * R, Rest...>(buf, tw + (NS > 1 ? NS : 0), tid);
 }
 
+// (PHD_COL_CLAMP=0: an A/B build with the column plans' passes unclamped)
+#ifndef PHD_COL_CLAMP
+#define PHD_COL_CLAMP 1
+#endif
 // Every pass but the last in LDS; Last::load/compute are left to the caller
 // (whose outputs, element b + k*N/R_last of round q, stay in registers).
 // Clamped passes (the column plans).
@@ -287,7 +291,7 @@ struct Plan {
     using Last = typename Plan<N, T, NS * R, Rest...>::Last;
     static constexpr int last_tw_offset = (NS > 1 ? NS : 0) + Plan<N, T, NS * R, Rest...>::last_tw_offset;
     __device__ static __forceinline__ void all_but_last(double2* buf, const double2* tw, int tid) {
-        using P = Pass<N, T, R, NS, true>;
+        using P = Pass<N, T, R, NS, PHD_COL_CLAMP != 0>;
         double2 v[P::ROUNDS][R];
         P::load(buf, v, tid);
         P::compute(v, tw, tid);
@@ -299,7 +303,7 @@ struct Plan {
 };
 template <int N, int T, int NS, int R>
 struct Plan<N, T, NS, R> {
-    using Last = Pass<N, T, R, NS, true>;
+    using Last = Pass<N, T, R, NS, PHD_COL_CLAMP != 0>;
     static constexpr int last_tw_offset = 0;
     __device__ static __forceinline__ void all_but_last(double2*, const double2*, int) {}
 };
