@@ -220,9 +220,16 @@ hipStream_t work_stream(Context* c, void* stream) {
     return c->stream;
 }
 
+// A growth frees the old buffer only once the device is idle (round 6, ADVICE
+// r5: a pinned or device block freed under an in-flight copy would be a
+// use-after-unmap; every entry point drains its streams before it returns,
+// so this is belt and braces, and growth is rare).
 bool ensure_device(void** p, size_t* cap, size_t need) {
     if (*cap >= need && *p) return true;
-    if (*p) (void)hipFree(*p);
+    if (*p) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(*p);
+    }
     *p = nullptr;
     *cap = 0;
     size_t sz = need + need / 4 + 4096;
@@ -237,7 +244,10 @@ bool ensure_device(void** p, size_t* cap, size_t need) {
 
 bool ensure_pinned(Context* c, size_t need) {
     if (c->pin_bytes >= need && c->h_pin) return true;
-    if (c->h_pin) (void)hipHostFree(c->h_pin);
+    if (c->h_pin) {
+        (void)hipDeviceSynchronize();
+        (void)hipHostFree(c->h_pin);
+    }
     c->h_pin = nullptr;
     size_t sz = need + need / 4 + 4096;
     if (hipHostMalloc(&c->h_pin, sz, hipHostMallocDefault) != hipSuccess) {
