@@ -41,6 +41,7 @@
 // one fp64 log of the mantissa product closes the run: e ln2 + log(m), as
 // pgm_normalize_fft's per-element fp64 log (src/fft_processing.c:196-199) to
 // ~1e-15 per run.  The max and the p >= 1 test stay in fp64.
+#include <algorithm>
 #include <cstdlib>
 
 // Nothing in this file needs the reference's rounding (the FFT only has to be
@@ -666,13 +667,22 @@ int resident_grid(K kernel, int threads, size_t lds) {
     return nb * num_cus();
 }
 
+// (timing builds: PHD_COL_BPC / PHD_ROW_BPC cap the persistent grids' blocks
+// per CU, so that two lanes' FFT passes can share the CUs -- the co-residency
+// study of round 6)
+static int bpc_cap(const char* knob, int g) {
+    const char* v = phd_knob(knob);
+    if (!v || atoi(v) < 1) return g;
+    return std::min(g, atoi(v) * num_cus());
+}
+
 template <int W, int T, int... Rs>
 hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, const double* k255,
                    const double2* tw, double2* inter, unsigned long long* rsum, hipStream_t st,
                    const uint8_t* const* imgs = nullptr, int nimg = 1, long istride = 0) {
     const size_t lds = RowK<W, T, Rs...>::lds;
     static const int grid = [&] {
-        const int g = resident_grid(k_rows_ct<W, T, Rs...>, T, lds) / 32 * 32;   // schedule needs % 32
+        const int g = bpc_cap("PHD_ROW_BPC", resident_grid(k_rows_ct<W, T, Rs...>, T, lds)) / 32 * 32;   // % 32
         return g > 32 ? g : 32;
     }();
     phd_launch((k_rows_ct<W, T, Rs...>), dim3(grid), dim3(T), lds, st, img, H, sums, k255, tw, inter,
@@ -682,7 +692,8 @@ hipError_t rows_ct(const uint8_t* img, int H, const unsigned long long* sums, co
 
 template <int H, int T, bool PF, int... Rs>
 int cols_grid_form() {
-    const int g = resident_grid(k_cols_ct<H, T, PF, Rs...>, T, ColK<H, T, PF, Rs...>::lds) / 32 * 32;   // XCD quads
+    const int g = bpc_cap("PHD_COL_BPC", resident_grid(k_cols_ct<H, T, PF, Rs...>, T, ColK<H, T, PF, Rs...>::lds)) /
+                  32 * 32;   // XCD quads
     return g < 32 ? 32 : g;
 }
 
