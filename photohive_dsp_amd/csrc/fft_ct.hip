@@ -67,6 +67,10 @@ typedef unsigned u32x3a __attribute__((ext_vector_type(3), aligned(4)));
 // a device array, and a generic (flat) load would also count against the LDS
 // counter, so every LDS wait of the FFT would wait for the prefetched pixels
 typedef const __attribute__((address_space(1))) u32x3a gu32x3a;
+// the row pass's pixel loads: non-temporal (PHD_ROW_NT=0: plain, an A/B build)
+#ifndef PHD_ROW_NT
+#define PHD_ROW_NT 1
+#endif
 
 __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
     const unsigned x = (b >> 2) == 0 ? w.x : ((b >> 2) == 1 ? w.y : w.z);   // b is a constant
@@ -257,8 +261,13 @@ __global__ __launch_bounds__(T, (RowK<W, T, Rs...>::MINW)) void k_rows_ct(const 
 #pragma unroll
         for (int j = 0; j < K::LR; j++) {
             const int g = (K::G4 % T == 0 || tid + j * T < K::G4) ? tid + j * T : 0;
+#if PHD_ROW_NT
             rg[j][0] = __builtin_nontemporal_load((gu32x3a*)(r0 + 12 * g));
             rg[j][1] = __builtin_nontemporal_load((gu32x3a*)(r1 + 12 * g));
+#else
+            rg[j][0] = *(gu32x3a*)(r0 + 12 * g);
+            rg[j][1] = *(gu32x3a*)(r1 + 12 * g);
+#endif
         }
     };
     int s = 0, im = 0, pr = 0;
