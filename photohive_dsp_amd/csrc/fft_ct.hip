@@ -67,9 +67,15 @@ typedef unsigned u32x3a __attribute__((ext_vector_type(3), aligned(4)));
 // a device array, and a generic (flat) load would also count against the LDS
 // counter, so every LDS wait of the FFT would wait for the prefetched pixels
 typedef const __attribute__((address_space(1))) u32x3a gu32x3a;
-// the row pass's pixel loads: non-temporal (PHD_ROW_NT=0: plain, an A/B build)
+// The row pass's pixel loads are plain loads (round 6; PHD_ROW_NT=1, an A/B
+// build, makes them non-temporal as before): a 12000-byte image row starts
+// 0-96 B into a 128-B line, so two wave-instructions share the line at each
+// 768-byte boundary, and the non-temporal first request let the stores'
+// traffic evict it before the second.  Rows 41.2-41.3 -> 39.2-39.6 us, their
+// HBM traffic 142.2 -> 137.2 MB per image (1.039x the algorithmic bytes;
+// profiles/r06/row_loads_temporal_ab.log).
 #ifndef PHD_ROW_NT
-#define PHD_ROW_NT 1
+#define PHD_ROW_NT 0
 #endif
 
 __device__ __forceinline__ int byte_of(const u32x3a& w, int b) {
