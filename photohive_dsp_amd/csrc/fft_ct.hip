@@ -109,36 +109,36 @@ __device__ __forceinline__ u32x3a rot_px(const u32x3a& w, int r) {
 
 // One thread's walk over E consecutive rows of a column: p per row in LDS
 // (lgb[r0 + j]), the column's bin runs in LDS (rl: start row << 16 | bin id,
-// ColRuns; rl[rlast] is a sentinel or past it, whose start is the height),
-// idx = the run holding row r0.  Contiguous rows of one bin form a run whose
-// sum of log p is the log of its product: the frexp mantissas multiply (>=
-// 2^-E, no underflow), the exponents add, and one fp64 log closes the run
-// (pgm_normalize_fft's fp64 log, src/fft_processing.c:196-199).  Each run adds
-// bin_scale fixed point to its run's LDS slot (sl, indexed like rl) with one
-// LDS atomic (order-independent sums); the block adds the column's slots to
-// the image's bins afterwards.
+// ColRuns), sg = the thread's segment word (ColBins::seg: the run holding row
+// r0, bits 0-7, and the rows j > 0 where a run starts, bit 8 + j).  Contiguous
+// rows of one bin form a run whose sum of log p is the log of its product: the
+// frexp mantissas multiply (>= 2^-E, no underflow), the exponents add, and one
+// fp64 log closes the run (pgm_normalize_fft's fp64 log, src/fft_processing.c:
+// 196-199).  Each run adds bin_scale fixed point to its run's LDS slot (sl,
+// indexed like rl) with one LDS atomic (order-independent sums); the block
+// adds the column's slots to the image's bins afterwards.
 //
 // Fast form (round 6), a wave whose lanes each meet at most two run starts
-// in their E rows (~97 % of the waves of 4000x3000 / 72x40,
-// tools/col_run_stats.py): branch-free, the starts r0 + f1, r0 + f2 of runs
-// idx + 1 and idx + 2 read from the run list, the product restarting at each
-// and the first two runs' products kept in registers; the wave then
-// evaluates the fp64 log two or three times.  Otherwise the general walk: the
-// run list's entries in registers, one branch per row (some lane of 64
-// changes bin on most rows).  Both multiply the same rows in the same order:
-// identical bins.  HFULL: H % E == 0, so a thread with r0 < H has all E rows.
+// (~97 % of the waves of 4000x3000 / 72x40): branch-free, the starts f1 < f2
+// from the segment word, the product restarting at each and the first two
+// runs' products kept in registers; the wave then evaluates the fp64 log two
+// or three times.  Otherwise the general walk: the run list's entries in
+// registers, one branch per row (some lane of 64 changes bin on most rows).
+// Both multiply the same rows in the same order: identical bins.
+// HFULL: H % E == 0, so a thread with r0 < H has all E rows.
 template <int E, bool HFULL>
 __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0, int rend, const unsigned* rl,
-                                          int idx, int rlast, unsigned long long* sl, double bscale,
+                                          unsigned sg, unsigned long long* sl, double bscale,
                                           const double2* __restrict__ lt) {
     auto flush = [&](int k, double m, int e) {
         const double acc = fmax((double)e * 0.69314718055994530942 + log_mant(m, lt), 0.0);
         atomicAdd(&sl[k], bin_fixed(acc, bscale));
     };
     if (r0 >= rend) return;
-    const int f1 = (int)(rl[min(idx + 1, rlast)] >> 16) - r0, f2 = (int)(rl[min(idx + 2, rlast)] >> 16) - r0;
-    const int f3 = (int)(rl[min(idx + 3, rlast)] >> 16) - r0;
-    if (__all(f3 >= E)) {
+    const int idx = (int)(sg & 255u);
+    const unsigned chm = sg >> 8;
+    if (__all(__popc(chm) <= 2)) {
+        const int f1 = __builtin_ctz(chm | 0x80000000u), f2 = __builtin_ctz((chm & (chm - 1)) | 0x80000000u);
         double mp = 1.0, m0 = 1.0, m1 = 1.0;
         int es = 0, e0 = 0, e1 = 0;
 #pragma unroll
@@ -160,7 +160,7 @@ __device__ __forceinline__ void walk_runs(const double* __restrict__ lgb, int r0
                 es += e;
             }
         }
-        const int n = (f1 < E ? 1 : 0) + (f2 < E ? 1 : 0);
+        const int n = __popc(chm);
         flush(idx, n == 0 ? mp : m0, n == 0 ? es : e0);
         if (n >= 1) flush(idx + 1, n == 1 ? mp : m1, n == 1 ? es : e1);
         if (n == 2) flush(idx + 2, mp, es);
@@ -480,7 +480,7 @@ __device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70)
 template <int H, int T, bool FULL, int... Rs>
 __global__ __launch_bounds__(T, (ColK<H, T, FULL, Rs...>::MINW)) void k_cols_ct(const double2* __restrict__ inter0, int wf,
                                                      const unsigned* __restrict__ runs,
-                                                     const uint8_t* __restrict__ segidx, int rstride,
+                                                     const unsigned* __restrict__ segidx, int rstride,
                                                      unsigned long long* __restrict__ bin_sums0, double* __restrict__ fmax_part0,
                                                      const double2* __restrict__ twg,
                                                      const unsigned long long* __restrict__ sums0, int width,
@@ -568,10 +568,10 @@ __global__ __launch_bounds__(T, (ColK<H, T, FULL, Rs...>::MINW)) void k_cols_ct(
         const int col = 2 * (2 * u + (quad >> 1)) + half;
         const bool live = col < wf;                       // the phantom column of an odd wf idles
         // the column's bin runs (image-independent, ~0.3 KB per column; ColRuns)
-        // and the run holding this thread's first row tid * E: loaded now, stored
+        // and this thread's segment word (walk_runs): loaded now, the list stored
         // to LDS after the FFT (a phantom column reads column 0's: its p are 1)
         unsigned rreg[K::RPT];
-        int sidx;
+        unsigned sidx;
         {
             const int rc = live ? col : 0;
             const unsigned* rsrc = runs + (size_t)rc * rstride;
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(T, (ColK<H, T, FULL, Rs...>::MINW)) void k_cols_ct(
         if (u + 1 < un && !pf_late) dma(u + 1, K::PF ? 0 : 1);
         // contiguous runs of one bin: one LDS atomic per run (bins change every
         // few tens of rows along a column; walk_runs)
-        if (!(ablate & 2)) walk_runs<K::E, H % K::E == 0>(lgb, tid * K::E, H, rl, sidx, min(rstride, kColRunsMax) - 1, sl, bscale, lt);
+        if (!(ablate & 2)) walk_runs<K::E, H % K::E == 0>(lgb, tid * K::E, H, rl, sidx, sl, bscale, lt);
         __syncthreads();
         if (!K::PF && u + 1 < un && !pf_late) dma(u + 1, 2);   // p is read: the lower half too
         // the column's run sums into the image's bins (a bin met by two runs of

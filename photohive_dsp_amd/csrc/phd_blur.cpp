@@ -128,27 +128,31 @@ bool build_col_runs(const uint16_t* map, int height, int wf, int T, ColRuns* r) 
         stride = std::max(stride, n + 1);                  // + the sentinel
     }
     r->max_entries = stride;
-    if (stride > kColRunsMax || H > 65535) {
+    // (E <= 24: a thread's run-start rows are bits 8 .. 31 of its segment word)
+    if (stride > kColRunsMax || H > 65535 || E > 24) {
         r->too_many = true;                                // a fixed property of the size: cached
         return false;
     }
     std::vector<uint32_t> runs((size_t)wf * stride, (uint32_t)H << 16);
-    std::vector<uint8_t> seg((size_t)wf * T, 0);
+    std::vector<uint32_t> seg((size_t)wf * T, 0u);
     for (int x = 0; x < wf; x++) {
         const uint16_t* col = map + (size_t)x * H;
         uint32_t* rl = runs.data() + (size_t)x * stride;
         int k = 0;
         for (int u = 0; u < H; u++) {
-            if (u == 0 || col[u] != col[u - 1]) rl[k++] = ((uint32_t)u << 16) | col[u];
-            // thread t's first row t E lies in run k - 1
-            if (u % E == 0) seg[(size_t)x * T + u / E] = (uint8_t)(k - 1);
+            const bool start = u == 0 || col[u] != col[u - 1];
+            if (start) rl[k++] = ((uint32_t)u << 16) | col[u];
+            // thread t's first row t E lies in run k - 1; a run starting at its
+            // row j > 0 sets bit 8 + j
+            if (u % E == 0) seg[(size_t)x * T + u / E] = (uint32_t)(k - 1);
+            else if (start) seg[(size_t)x * T + u / E] |= 1u << (8 + u % E);
         }
         rl[k] = (uint32_t)H << 16;                         // sentinel (its bin is never read)
     }
     if (hipMalloc(&r->d_runs, runs.size() * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&r->d_seg, seg.size()) != hipSuccess ||
+        hipMalloc(&r->d_seg, seg.size() * sizeof(uint32_t)) != hipSuccess ||
         hipMemcpy(r->d_runs, runs.data(), runs.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(r->d_seg, seg.data(), seg.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(r->d_seg, seg.data(), seg.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
         set_error("upload of the column bin runs failed");
         if (r->d_runs) (void)hipFree(r->d_runs);
         if (r->d_seg) (void)hipFree(r->d_seg);

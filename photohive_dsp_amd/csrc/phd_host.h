@@ -83,7 +83,7 @@ struct BlurTable {
 struct ColRuns {
     int T = 0, stride = 0;               // threads per column; entries per column (runs + sentinel)
     uint32_t* d_runs = nullptr;          // device [wf][stride]
-    uint8_t* d_seg = nullptr;            // device [wf][T]
+    uint32_t* d_seg = nullptr;           // device [wf][T]: run index | run-start rows << 8 (ColBins::seg)
     int max_entries = 0;                 // the longest column's runs + sentinel
     bool too_many = false;               // max_entries > kColRunsMax: runtime-plan FFT for this size
 };

@@ -344,7 +344,9 @@ inline size_t inter_elems(int height, int width) {
 constexpr int kColRunsMax = 256;   // entries (runs + sentinel) of one column's list (LDS)
 struct ColBins {
     const uint32_t* runs = nullptr;  // [wf][rstride] runs of one polar bin (ColRuns, phd_host.h)
-    const uint8_t* seg = nullptr;    // [wf][T] the run holding each thread's first row
+    // [wf][T] per thread: the run holding its first row (bits 0-7) and the rows
+    // j = 1 .. E-1 of its E where a run starts (bit 8 + j; E <= 24)
+    const uint32_t* seg = nullptr;
     int rstride = 0;                 // entries per column
 };
 size_t fft_cols_ct_lds(int height);
