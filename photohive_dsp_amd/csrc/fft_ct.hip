@@ -430,7 +430,13 @@ struct ColK {
     static constexpr int BPC1 = (int)((160 * 1024) / (sizeof(double2) * (H + NTW) + 1024)) < 2 ? 1 : 2;
     // (round 6: 3000 rows at 320 threads, three passes, needs three waves per
     // SIMD for two blocks, i.e. 168 VGPRs: 50-60 spilled; not pursued)
+#ifdef PHD_COL_MINW3
+    // (A/B build: the 3000-row half-prefetch form at three waves per SIMD,
+    // three blocks per CU in its 54.2 KB of LDS; 168 VGPRs, ~66 spilled)
+    static constexpr int MINW = (H == 3000 && !FULL) ? 3 : (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2;
+#else
     static constexpr int MINW = (T >= 512 ? 4 : (T >= 384 ? 3 : 2)) * BPC1 / 2;
+#endif
     // The next column streams into the column buffer by LDS-DMA (no
     // registers) while the current one finishes (round 5).
     //  * Full-prefetch form (PF): p per row gets an LDS array of its own, so
