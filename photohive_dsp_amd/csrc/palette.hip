@@ -72,6 +72,18 @@ __device__ __forceinline__ void load4(const uint8_t* __restrict__ img, long p0, 
 typedef const __attribute__((address_space(1))) unsigned gu32;   // global (not flat) loads
 
 __device__ __forceinline__ int px_byte(const unsigned (&w)[3], int b) { return (w[b >> 2] >> (8 * (b & 3))) & 255; }
+// One of four words by a runtime index, from values the compiler cannot trace
+// back to a register array (it would turn the selects into a dynamically
+// indexed array, i.e. scratch memory)
+__device__ __forceinline__ unsigned sel4_opaque(int k, unsigned a, unsigned b, unsigned c, unsigned d) {
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+}
+// pixel i (runtime, 0-3) of a 4-pixel group's words w0 w1 w2 in bits 0-23
+__device__ __forceinline__ unsigned px_word(unsigned w0, unsigned w1, unsigned w2, int i) {
+    const unsigned p1 = __builtin_amdgcn_alignbyte(w1, w0, 3u), p2 = __builtin_amdgcn_alignbyte(w2, w1, 2u);
+    return i == 0 ? w0 : (i == 1 ? p1 : (i == 2 ? p2 : w2 >> 8));
+}
 
 // Add one to lds[g] for every lane with g >= 0; a wave whose lanes all hit the
 // same group issues one atomic (flat regions of real images).
@@ -1093,8 +1105,17 @@ __global__ __launch_bounds__(kPartThreads) void k_partial_sums_img(
             const int bt = __ffs(cand) - 1;
             cand &= cand - 1;
             const int st = bt >> 2, i = bt & 3;
-            add(ub + 4L * tid + 4L * kPartThreads * st + i, px_byte(x.w[st], 3 * i), px_byte(x.w[st], 3 * i + 1),
-                px_byte(x.w[st], 3 * i + 2));
+            // the group's words and the pixel's bytes by selects: a register
+            // array indexed by a runtime st or byte put the unit in scratch
+            // memory (round 6), and a kernel with scratch stalls the other
+            // lane's concurrent kernels
+            unsigned ws[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                ws[k] = sel4_opaque(st, x.w[0][k], x.w[1][k], x.w[2][k], x.w[3][k]);
+            const unsigned pw = px_word(ws[0], ws[1], ws[2], i);
+            add(ub + 4L * tid + 4L * kPartThreads * st + i, (int)(pw & 255u), (int)((pw >> 8) & 255u),
+                (int)((pw >> 16) & 255u));
         }
     };
     // two units in flight: the next one's loads are issued before this one's
