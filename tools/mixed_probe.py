@@ -1,7 +1,7 @@
 """Per-size cost of the full report (config 5 sizes): for each shape in
 shard.MIXED_SHAPES, a batch of n device-resident images through
 phd_report_batch_device, wall time and per-kernel HIP-event averages.
-Usage: python tools/mixed_probe.py [n] [h s v]"""
+Usage: python tools/mixed_probe.py [n] [h s v]   (PROBE_SHAPES=HxW,..., PROBE_KIND=hblur, PROBE_HSV=h,s,v)"""
 import ctypes
 import json
 import os
@@ -16,7 +16,8 @@ from photohive_dsp_amd.lib import lib, last_error  # noqa: E402
 from photohive_dsp_amd.structures import Full_Report_Data  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-hsv = [int(x) for x in sys.argv[2:5]] if len(sys.argv) > 4 else [36, 4, 5]
+hsv = ([int(x) for x in sys.argv[2:5]] if len(sys.argv) > 4 else
+       [int(x) for x in os.environ["PROBE_HSV"].split(",")] if os.environ.get("PROBE_HSV") else [36, 4, 5])
 cfg = make_config(h_partitions=hsv[0], s_partitions=hsv[1], v_partitions=hsv[2])
 names = ["k1", "fft_rows", "fft_cols", "cutoffs", "pal_sums", "sharp"]
 shapes = sorted(set(shard.MIXED_SHAPES), key=lambda s: s[0] * s[1])
@@ -26,7 +27,10 @@ for h, w in shapes:
     nb = 3 * h * w
     t = torch.empty(n * nb, dtype=torch.uint8, device="cuda")
     for i in range(n):
-        assert lib.phd_fill_uniform_device(t[i * nb:].data_ptr(), nb, 77 + i, None) == 0
+        if os.environ.get("PROBE_KIND") == "hblur":       # bench.py's structured images
+            assert lib.phd_fill_structured_device(t[i * nb:].data_ptr(), h, w, 2 + i, 15, 1, None) == 0
+        else:
+            assert lib.phd_fill_uniform_device(t[i * nb:].data_ptr(), nb, 77 + i, None) == 0
     outs = (ctypes.POINTER(Full_Report_Data) * n)()
     st = (ctypes.c_int * n)()
 
