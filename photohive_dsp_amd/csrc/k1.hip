@@ -481,7 +481,11 @@ __global__ __launch_bounds__(KT, 4) void k_k1t(const uint8_t* const* __restrict_
             p2 = q[2];
         }
         __syncthreads();
+#if defined(PHD_K1_MERGE_DEN)
+        merge = PHD_K1_MERGE_DEN * vote[16 * vpar] > (unsigned)(kT * kG);   // A/B builds: other thresholds
+#else
         merge = 5 * vote[16 * vpar] > (unsigned)(kT * kG);       // the next chunk's mode: > 1/5 of groups
+#endif
         // fold the chunk's count words: one thread per cell sums its C copies;
         // the run's cell counts, the chunk's group counts, per-group sum kmax / n255
 #if defined(PHD_K1_ABL_NOFOLD)
