@@ -259,6 +259,18 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
         }
         const K1Px p = k1_pixel_x<SMALL>((int)((Xp[q] >> sh) & 0xFFFF), special, kmx, kmn, kd, ce[i], ekd[i], G);
         if constexpr (MERGE) {
+#if defined(PHD_K1_MERGE_SEL)
+            // (A/B build) the run update by selects, only the flush's atomics
+            // under a branch; the same sums (0 + x = x exactly)
+            const bool same = p.cell == run->cell;
+            if (!same && run->cell >= 0) acc_add(A, run->cell, run->grp, run->lo, run->hi, run->h, run->s);
+            run->lo = (same ? run->lo : 0u) + p.lo;
+            run->hi = (same ? run->hi : 0u) + p.hi;
+            run->h = (same ? run->h : 0.0) + p.h;
+            run->s = (same ? run->s : 0.0) + p.s;
+            run->cell = p.cell;
+            run->grp = p.grp;
+#else
             if (p.cell == run->cell) {
                 run->lo += p.lo;
                 run->hi += p.hi;
@@ -268,6 +280,7 @@ __device__ __forceinline__ unsigned k1_group(unsigned w0, unsigned w1, unsigned 
                 if (run->cell >= 0) acc_add(A, run->cell, run->grp, run->lo, run->hi, run->h, run->s);
                 *run = CellRun{p.cell, p.grp, p.lo, p.hi, p.h, p.s};
             }
+#endif
         } else {
             acc_add(A, p);
         }

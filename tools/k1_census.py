@@ -64,11 +64,15 @@ def loops(lines):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
+    ap.add_argument("--asm", default=None, help="an already compiled k1.s (e.g. an A/B build's flags)")
     a = ap.parse_args()
-    with tempfile.TemporaryDirectory() as d:
-        s = os.path.join(d, "k1.s")
-        subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + ["-o", s, SRC], check=True)
-        text = open(s).read().splitlines()
+    if a.asm:
+        text = open(a.asm).read().splitlines()
+    else:
+        with tempfile.TemporaryDirectory() as d:
+            s = os.path.join(d, "k1.s")
+            subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + ["-o", s, SRC], check=True)
+            text = open(s).read().splitlines()
     # split by function
     funcs = collections.OrderedDict()
     cur = None
